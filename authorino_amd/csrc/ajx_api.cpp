@@ -1,0 +1,243 @@
+// ajx_api.cpp — the C-ABI (include/authjx.h): device contexts, reconcile-time compile
+// into HBM-resident rulesets, batch evaluation.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/authjx.h"
+#include "ajx_compiler.h"
+#include "ajx_kernels.h"
+
+struct authjx_ruleset {
+    int device = 0;
+    uint8_t* d_blob = nullptr;
+    ajx::CompiledRuleset c;
+};
+
+struct authjx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::mutex mu;        // serialises device-side calls on this context (set table)
+    std::mutex batch_mu;  // serialises authjx_eval_batch (owns the staging buffer)
+    // device set table: pointers to ruleset blobs
+    const uint8_t** d_sets = nullptr;
+    uint32_t sets_cap = 0;
+    std::vector<const uint8_t*> last_sets;
+    const uint8_t** h_sets_pinned = nullptr;
+    // staging for authjx_eval_batch (host buffers)
+    uint8_t* d_stage = nullptr;
+    size_t stage_cap = 0;
+    float last_ms = 0.f;
+};
+
+namespace {
+
+#define HIP_OK(x)                                   \
+    do {                                            \
+        hipError_t e_ = (x);                        \
+        if (e_ != hipSuccess) return AUTHJX_EDEVICE; \
+    } while (0)
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int ensure_sets(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets, hipStream_t stream) {
+    std::vector<const uint8_t*> ptrs(n_sets);
+    for (uint32_t i = 0; i < n_sets; i++) {
+        if (!sets[i] || sets[i]->device != ctx->device) return AUTHJX_EINVAL;
+        ptrs[i] = sets[i]->d_blob;
+    }
+    if (ptrs == ctx->last_sets) return AUTHJX_OK;
+    if (n_sets > ctx->sets_cap) {
+        if (ctx->d_sets) (void)hipFree(ctx->d_sets);
+        if (ctx->h_sets_pinned) (void)hipHostFree(ctx->h_sets_pinned);
+        ctx->d_sets = nullptr;
+        ctx->h_sets_pinned = nullptr;
+        uint32_t cap = n_sets < 64 ? 64 : n_sets;
+        HIP_OK(hipMalloc(&ctx->d_sets, cap * sizeof(uint8_t*)));
+        HIP_OK(hipHostMalloc(&ctx->h_sets_pinned, cap * sizeof(uint8_t*), hipHostMallocDefault));
+        ctx->sets_cap = cap;
+    }
+    // the pinned table may still be read by an in-flight copy of the previous batch
+    HIP_OK(hipStreamSynchronize(stream));
+    std::memcpy(ctx->h_sets_pinned, ptrs.data(), n_sets * sizeof(uint8_t*));
+    HIP_OK(hipMemcpyAsync(ctx->d_sets, ctx->h_sets_pinned, n_sets * sizeof(uint8_t*), hipMemcpyHostToDevice, stream));
+    ctx->last_sets = ptrs;
+    return AUTHJX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int authjx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int authjx_init(int device, authjx_ctx** out) {
+    if (!out) return AUTHJX_EINVAL;
+    *out = nullptr;
+    int n = authjx_device_count();
+    if (device < 0 || device >= n) return AUTHJX_EDEVICE;
+    HIP_OK(hipSetDevice(device));
+    authjx_ctx* c = new authjx_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return AUTHJX_EDEVICE;
+    }
+    *out = c;
+    return AUTHJX_OK;
+}
+
+void authjx_shutdown(authjx_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_sets) (void)hipFree(ctx->d_sets);
+    if (ctx->h_sets_pinned) (void)hipHostFree(ctx->h_sets_pinned);
+    if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int authjx_compile(authjx_ctx* ctx, const authjx_tree* tree, authjx_ruleset** out, int32_t* pattern_status,
+                   char* errbuf, size_t errcap) {
+    if (!ctx || !tree || !out) return AUTHJX_EINVAL;
+    *out = nullptr;
+    authjx_ruleset* rs = new authjx_ruleset();
+    std::string err;
+    int rc = ajx::compile_tree(tree, &rs->c, &err);
+    if (errbuf && errcap) std::snprintf(errbuf, errcap, "%s", err.c_str());
+    if (rc != AUTHJX_OK) {
+        delete rs;
+        return rc;
+    }
+    if (pattern_status)
+        for (uint32_t i = 0; i < rs->c.n_patterns; i++) pattern_status[i] = rs->c.pattern_status[i];
+    rs->device = ctx->device;
+    if (hipSetDevice(ctx->device) != hipSuccess ||
+        hipMalloc(&rs->d_blob, rs->c.blob.size()) != hipSuccess ||
+        hipMemcpy(rs->d_blob, rs->c.blob.data(), rs->c.blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        if (rs->d_blob) (void)hipFree(rs->d_blob);
+        delete rs;
+        return AUTHJX_EDEVICE;
+    }
+    *out = rs;
+    return AUTHJX_OK;
+}
+
+void authjx_free(authjx_ruleset* rs) {
+    if (!rs) return;
+    if (rs->d_blob) {
+        (void)hipSetDevice(rs->device);
+        (void)hipDeviceSynchronize();  // no batch may still read the blob
+        (void)hipFree(rs->d_blob);
+    }
+    delete rs;
+}
+
+uint32_t authjx_ruleset_patterns(const authjx_ruleset* rs) { return rs ? rs->c.n_patterns : 0; }
+uint32_t authjx_ruleset_selectors(const authjx_ruleset* rs) { return rs ? rs->c.n_selectors : 0; }
+
+size_t authjx_pattern_error(const authjx_ruleset* rs, uint32_t i, char* buf, size_t cap) {
+    if (!rs || i >= rs->c.n_patterns) return 0;
+    const std::string& e = rs->c.pattern_error[i];
+    if (buf && cap) std::snprintf(buf, cap, "%s", e.c_str());
+    return e.size();
+}
+
+int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                             const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
+                             const uint32_t* d_lens, uint32_t n, uint8_t* d_out_tristate, int32_t* d_out_err_idx,
+                             uint64_t* d_out_bitmap, uint32_t bitmap_stride_words, void* stream) {
+    if (!ctx || !sets || n_sets == 0 || (n && (!d_arena || !d_offs || !d_lens || !d_out_tristate)))
+        return AUTHJX_EINVAL;
+    if (n_sets > 1 && !d_set_of_req) return AUTHJX_EINVAL;
+    uint32_t need_words = 0;
+    for (uint32_t i = 0; i < n_sets; i++) {
+        if (!sets[i]) return AUTHJX_EINVAL;
+        uint32_t w = (sets[i]->c.n_patterns + 63) / 64;
+        if (w > need_words) need_words = w;
+    }
+    if (d_out_bitmap && bitmap_stride_words < need_words) return AUTHJX_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_OK(hipSetDevice(ctx->device));
+    int rc = ensure_sets(ctx, sets, n_sets, s);
+    if (rc != AUTHJX_OK) return rc;
+    HIP_OK(hipEventRecord(ctx->ev0, s));
+    HIP_OK(ajx::launch_eval_scan(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
+                                 d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
+    HIP_OK(hipEventRecord(ctx->ev1, s));
+    return AUTHJX_OK;
+}
+
+float authjx_last_kernel_ms(authjx_ctx* ctx) {
+    if (!ctx) return 0.f;
+    float ms = 0.f;
+    if (hipEventSynchronize(ctx->ev1) != hipSuccess) return 0.f;
+    if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return 0.f;
+    return ms;
+}
+
+int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                      const uint32_t* set_of_req, const uint8_t* arena, uint64_t arena_len, const uint64_t* offs,
+                      const uint32_t* lens, uint32_t n, uint8_t* out_tristate, int32_t* out_err_idx,
+                      uint64_t* out_bitmap, uint32_t bitmap_stride_words) {
+    if (!ctx || (n && (!arena || !offs || !lens || !out_tristate))) return AUTHJX_EINVAL;
+    for (uint32_t r = 0; r < n; r++)
+        if (offs[r] + lens[r] > arena_len) return AUTHJX_EINVAL;
+    const bool with_sor = set_of_req != nullptr;
+    size_t o_arena = 0;
+    size_t o_offs = round_up(o_arena + arena_len, 256);
+    size_t o_lens = round_up(o_offs + (size_t)n * 8, 256);
+    size_t o_sor = round_up(o_lens + (size_t)n * 4, 256);
+    size_t o_tri = round_up(o_sor + (with_sor ? (size_t)n * 4 : 0), 256);
+    size_t o_err = round_up(o_tri + (size_t)n, 256);
+    size_t o_bm = round_up(o_err + (size_t)n * 4, 256);
+    size_t total = round_up(o_bm + (out_bitmap ? (size_t)n * bitmap_stride_words * 8 : 0), 256);
+    std::lock_guard<std::mutex> batch_lock(ctx->batch_mu);
+    {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        HIP_OK(hipSetDevice(ctx->device));
+        if (total > ctx->stage_cap) {
+            if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+            ctx->d_stage = nullptr;
+            ctx->stage_cap = 0;
+            HIP_OK(hipMalloc(&ctx->d_stage, total));
+            ctx->stage_cap = total;
+        }
+        uint8_t* b = ctx->d_stage;
+        hipStream_t s = ctx->stream;
+        HIP_OK(hipMemcpyAsync(b + o_arena, arena, arena_len, hipMemcpyHostToDevice, s));
+        HIP_OK(hipMemcpyAsync(b + o_offs, offs, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        HIP_OK(hipMemcpyAsync(b + o_lens, lens, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        if (with_sor) HIP_OK(hipMemcpyAsync(b + o_sor, set_of_req, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    }
+    uint8_t* b = ctx->d_stage;
+    int rc = authjx_eval_batch_device(ctx, sets, n_sets, with_sor ? (const uint32_t*)(b + o_sor) : nullptr,
+                                      b + o_arena, (const uint64_t*)(b + o_offs), (const uint32_t*)(b + o_lens), n,
+                                      b + o_tri, out_err_idx ? (int32_t*)(b + o_err) : nullptr,
+                                      out_bitmap ? (uint64_t*)(b + o_bm) : nullptr, bitmap_stride_words, nullptr);
+    if (rc != AUTHJX_OK) return rc;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    hipStream_t s = ctx->stream;
+    HIP_OK(hipMemcpyAsync(out_tristate, b + o_tri, n, hipMemcpyDeviceToHost, s));
+    if (out_err_idx) HIP_OK(hipMemcpyAsync(out_err_idx, b + o_err, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (out_bitmap)
+        HIP_OK(hipMemcpyAsync(out_bitmap, b + o_bm, (size_t)n * bitmap_stride_words * 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return AUTHJX_OK;
+}
+
+}  // extern "C"

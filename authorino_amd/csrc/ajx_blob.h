@@ -1,0 +1,94 @@
+// ajx_blob.h — layout of a compiled ruleset as it sits in HBM (one contiguous blob per
+// ruleset, written by the reconcile-time compiler, read by the kernels).
+//
+// A ruleset is one jsonexp.Expression (pkg/jsonexp/expressions.go:102-104) compiled at
+// the point the reference builds it (controllers/auth_config_controller.go:805-852):
+//   selectors   deduplicated gjson paths, split into components the way gjson v1.14.0
+//               parseObjectPath / parseArrayPath split them (escapes removed for object
+//               keys, numeric index for arrays)
+//   patterns    (selector, op, literal, dfa) per jsonexp.Pattern
+//   code        fold bytecode of the And/Or tree: right-nested All/Any chains are
+//               flattened to n-ary AND/OR nodes whose value is the first child value
+//               that is not the node's identity (T for AND, F for OR) — exactly the
+//               short-circuit results of And.Matches :111-125 / Or.Matches :136-154
+//   literals    byte pool (component keys, pattern values)
+//   dfas        Go-regexp DFAs over rune classes (one per `matches` pattern)
+#pragma once
+#include <stdint.h>
+
+namespace ajx {
+
+constexpr uint32_t kMagic = 0x414A5842u;  // "AJXB"
+constexpr uint32_t kMaxComponents = 16;    // selector depth compiled for the device
+constexpr uint32_t kMaxDepth = 16;         // AND/OR nesting depth of the fold code
+constexpr uint32_t kMaxDfaStates = 4096;
+constexpr uint32_t kMaxDfaClasses = 255;
+
+// gjson.Type
+enum : uint8_t { T_NULL = 0, T_FALSE = 1, T_NUMBER = 2, T_STRING = 3, T_TRUE = 4, T_JSON = 5 };
+// tri-state values (= AUTHJX_F/T/E/UNDECIDED)
+enum : uint8_t { V_F = 0, V_T = 1, V_E = 2, V_U = 3 };
+// pattern state
+enum : uint8_t { P_OK = 0, P_STATIC_E = 1, P_UNSUPPORTED = 2 };
+// ops (= AUTHJX_OP_*)
+enum : uint8_t { OP_UNKNOWN = 0, OP_EQ = 1, OP_NEQ = 2, OP_INCL = 3, OP_EXCL = 4, OP_MATCHES = 5 };
+// fold code (op in bits 24..31, argument in bits 0..23)
+enum : uint32_t { C_OPEN_AND = 1, C_OPEN_OR = 2, C_PAT = 3, C_CLOSE = 4, C_CONST_T = 5, C_CONST_F = 6 };
+
+struct Component {
+    uint32_t lit_off;     // object-key bytes (escapes removed) in the literal pool
+    uint32_t lit_len;
+    int32_t array_index;  // element index when the value is an array, -1 = never
+    uint32_t hash;        // FNV-1a of the key bytes
+};
+
+struct Selector {
+    uint32_t comp_begin;
+    uint32_t comp_count;
+};
+
+struct Pattern {
+    uint32_t selector;
+    uint8_t op;
+    uint8_t state;
+    uint16_t pad;
+    uint32_t lit_off;
+    uint32_t lit_len;
+    uint32_t dfa_off;  // byte offset of a DfaHdr in the blob (0 = none)
+};
+
+struct DfaHdr {
+    uint32_t n_states;
+    uint32_t n_classes;
+    uint32_t start;
+    uint32_t match_state;  // absorbing accept
+    uint32_t trans_off;    // uint16_t[n_states * n_classes], blob offset
+    uint32_t eot_off;      // uint8_t[n_states]: accept at end of text
+    uint32_t ranges_off;   // RuneRange[n_ranges] for runes >= 0x80, sorted by lo
+    uint32_t n_ranges;
+    uint8_t ascii_class[128];
+};
+
+struct RuneRange {
+    uint32_t lo, hi, cls, pad;
+};
+
+struct RulesetHdr {
+    uint32_t magic;
+    uint32_t total_bytes;
+    uint32_t n_patterns;
+    uint32_t n_selectors;
+    uint32_t n_code;
+    uint32_t max_depth;
+    uint32_t off_selectors;
+    uint32_t off_components;
+    uint32_t off_patterns;
+    uint32_t off_code;
+    uint32_t off_literals;
+    uint32_t lit_bytes;
+    uint32_t n_components;
+    uint32_t flags;  // bit0: has regex; bit1: has unsupported pattern
+    uint32_t pad[2];
+};
+
+}  // namespace ajx

@@ -1,0 +1,322 @@
+// ajx_compiler.cpp — jsonexp tree -> ruleset blob (see ajx_blob.h for the layout).
+#include "ajx_compiler.h"
+
+#include <cstring>
+#include <functional>
+#include <map>
+
+#include "ajx_regex.h"
+
+namespace ajx {
+
+namespace {
+
+uint32_t fnv1a(const std::string& s) {
+    uint32_t h = 2166136261u;
+    for (unsigned char c : s) {
+        h ^= c;
+        h *= 16777619u;
+    }
+    return h;
+}
+
+// gjson parseUint on the raw array-context part; -1 when it can never equal an index
+int32_t array_index_of(const std::string& raw) {
+    if (raw.empty()) return -1;
+    uint64_t v = 0;
+    for (char c : raw) {
+        if (c < '0' || c > '9') return -1;
+        v = v * 10 + (uint64_t)(c - '0');  // wraps like Go's uint64
+    }
+    int64_t iv = (int64_t)v;  // int(n)
+    if (iv < 0 || iv > 0x7fffffff) return -1;
+    return (int32_t)iv;
+}
+
+}  // namespace
+
+bool split_selector(const std::string& p, std::vector<PathComponent>* out) {
+    out->clear();
+    const size_t n = p.size();
+    // gjson.Get special forms: modifiers '@', static '!', multipaths '[' '{', JSON lines '..'
+    if (n > 1 && (p[0] == '@' || p[0] == '!' || p[0] == '[' || p[0] == '{')) return false;
+    if (n >= 2 && p[0] == '.' && p[1] == '.') return false;
+    for (size_t i = 0; i < n; i++) {
+        char c = p[i];
+        if (c == '\\') {
+            i++;
+            if (i < n && (p[i] == '|' || p[i] == '#')) return false;  // special in array context
+            continue;
+        }
+        if (c == '|' || c == '#' || c == '*' || c == '?') return false;
+        if (c == '.' && i + 1 < n && (p[i + 1] == '@' || p[i + 1] == '[' || p[i + 1] == '{')) return false;
+    }
+    // parseObjectPath repeatedly on the remainder
+    size_t pos = 0;
+    for (;;) {
+        PathComponent comp;
+        std::string part;
+        size_t i = pos;
+        bool more = false, escaped = false;
+        size_t next = n;
+        for (; i < n; i++) {
+            char c = p[i];
+            if (c == '.') {
+                more = true;
+                next = i + 1;
+                break;
+            }
+            if (c == '\\') {
+                escaped = true;
+                i++;
+                if (i < n) part.push_back(p[i]);  // a trailing lone backslash is dropped
+                continue;
+            }
+            part.push_back(c);
+        }
+        // array context (parseArrayPath): raw text up to the first '.', no escape handling
+        size_t dot = p.find('.', pos);
+        std::string raw = p.substr(pos, (dot == std::string::npos ? n : dot) - pos);
+        comp.key = part;
+        comp.array_index = escaped && raw.find('\\') != std::string::npos ? -1 : array_index_of(raw);
+        out->push_back(comp);
+        if (!more) break;
+        pos = next;
+    }
+    return out->size() <= kMaxComponents;
+}
+
+namespace {
+
+struct NormNode {
+    int kind;  // 0 = AND, 1 = OR, 2 = leaf pattern, 3 = const T, 4 = const F
+    int pattern = -1;
+    std::vector<NormNode> kids;
+};
+
+struct Builder {
+    std::vector<uint8_t> blob;
+    size_t align16() {
+        while (blob.size() % 16) blob.push_back(0);
+        return blob.size();
+    }
+    size_t append(const void* p, size_t n) {
+        size_t off = blob.size();
+        blob.resize(off + n);
+        if (n) std::memcpy(blob.data() + off, p, n);
+        return off;
+    }
+};
+
+}  // namespace
+
+int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err) {
+    if (!tree) return AUTHJX_EINVAL;
+    const uint32_t np = tree->n_patterns, nn = tree->n_nodes;
+    if ((np && !tree->patterns) || (nn && !tree->nodes)) return AUTHJX_EINVAL;
+    if (tree->root >= (int32_t)nn) return AUTHJX_EINVAL;
+
+    // ---- normalise the And/Or tree into n-ary fold nodes ----
+    std::vector<int> visiting(nn, 0);
+    bool bad = false;
+    std::function<void(int, int, std::vector<NormNode>*)> gather;
+    std::function<NormNode(int)> norm = [&](int idx) -> NormNode {
+        const authjx_node& nd = tree->nodes[idx];
+        if (nd.kind == AUTHJX_NODE_PATTERN) {
+            if (nd.pattern < 0 || (uint32_t)nd.pattern >= np) { bad = true; return NormNode{3}; }
+            NormNode l{2};
+            l.pattern = nd.pattern;
+            return l;
+        }
+        if (nd.kind != AUTHJX_NODE_AND && nd.kind != AUTHJX_NODE_OR) { bad = true; return NormNode{3}; }
+        int k = nd.kind == AUTHJX_NODE_AND ? 0 : 1;
+        NormNode r{k};
+        gather(idx, k, &r.kids);
+        if (r.kids.empty()) return NormNode{k == 0 ? 3 : 4};  // And{} = T, Or{} = F
+        if (r.kids.size() == 1) return r.kids[0];
+        return r;
+    };
+    // flatten same-kind descendants (fold is associative), skipping nil sides
+    gather = [&](int idx, int k, std::vector<NormNode>* kids) {
+        if (bad) return;
+        if (visiting[(size_t)idx]) { bad = true; return; }
+        visiting[(size_t)idx] = 1;
+        const authjx_node& nd = tree->nodes[idx];
+        for (int child : {nd.left, nd.right}) {
+            if (child < 0) continue;
+            if ((uint32_t)child >= nn) { bad = true; break; }
+            const authjx_node& cn = tree->nodes[child];
+            int ck = cn.kind == AUTHJX_NODE_AND ? 0 : cn.kind == AUTHJX_NODE_OR ? 1 : -1;
+            if (ck == k) {
+                gather(child, k, kids);
+            } else {
+                if (visiting[(size_t)child]) { bad = true; break; }
+                kids->push_back(norm(child));
+            }
+        }
+        visiting[(size_t)idx] = 0;
+    };
+    NormNode root = tree->root < 0 ? NormNode{3} : norm(tree->root);
+    if (bad) {
+        if (err) *err = "malformed expression tree";
+        return AUTHJX_EINVAL;
+    }
+
+    std::vector<uint32_t> code;
+    uint32_t max_depth = 0;
+    std::function<void(const NormNode&, uint32_t)> emit = [&](const NormNode& n, uint32_t depth) {
+        switch (n.kind) {
+            case 2: code.push_back((C_PAT << 24) | (uint32_t)n.pattern); return;
+            case 3: code.push_back(C_CONST_T << 24); return;
+            case 4: code.push_back(C_CONST_F << 24); return;
+            default:
+                max_depth = std::max(max_depth, depth + 1);
+                code.push_back((n.kind == 0 ? C_OPEN_AND : C_OPEN_OR) << 24);
+                for (const NormNode& c : n.kids) emit(c, depth + 1);
+                code.push_back(C_CLOSE << 24);
+        }
+    };
+    emit(root, 0);
+    if (max_depth > kMaxDepth) {
+        if (err) *err = "expression nests And/Or deeper than the device fold stack";
+        return AUTHJX_ELIMIT;
+    }
+    if (np > 0xFFFFFF) return AUTHJX_ELIMIT;
+
+    // ---- selectors, patterns, literals, DFAs ----
+    std::string lits;
+    std::map<std::string, uint32_t> sel_ids;
+    std::vector<Selector> sels;
+    std::vector<Component> comps;
+    std::vector<Pattern> pats(np);
+    std::vector<RegexDfa> dfas;
+    std::vector<int> dfa_of(np, -1);
+    out->pattern_status.assign(np, AUTHJX_PAT_OK);
+    out->pattern_error.assign(np, "");
+    uint32_t flags = 0;
+    for (uint32_t i = 0; i < np; i++) {
+        const authjx_pattern& ap = tree->patterns[i];
+        std::string sel(ap.selector ? ap.selector : "", ap.selector_len);
+        std::string val(ap.value ? ap.value : "", ap.value_len);
+        Pattern& p = pats[i];
+        std::memset(&p, 0, sizeof p);
+        p.op = (uint8_t)(ap.op >= 0 && ap.op <= 5 ? ap.op : 0);
+        p.lit_off = (uint32_t)lits.size();
+        p.lit_len = (uint32_t)val.size();
+        lits += val;
+        // Pattern.Matches: the operator decides first whether an error is returned
+        if (ap.op < AUTHJX_OP_EQ || ap.op > AUTHJX_OP_MATCHES) {
+            p.state = P_STATIC_E;
+            out->pattern_status[i] = AUTHJX_PAT_STATIC_ERROR;
+            out->pattern_error[i] = "unsupported operator for json authorization";
+            continue;
+        }
+        if (ap.op == AUTHJX_OP_MATCHES) {
+            RegexDfa dfa;
+            std::string rerr;
+            RegexStatus st = compile_go_regex(val, &dfa, &rerr);
+            if (st == RX_ERROR) {
+                p.state = P_STATIC_E;
+                out->pattern_status[i] = AUTHJX_PAT_STATIC_ERROR;
+                out->pattern_error[i] = rerr;
+                continue;
+            }
+            if (st == RX_UNSUPPORTED) {
+                p.state = P_UNSUPPORTED;
+                out->pattern_status[i] = AUTHJX_PAT_UNSUPPORTED;
+                out->pattern_error[i] = rerr;
+                flags |= 2;
+                continue;
+            }
+            dfa_of[i] = (int)dfas.size();
+            dfas.push_back(std::move(dfa));
+            flags |= 1;
+        }
+        auto it = sel_ids.find(sel);
+        if (it == sel_ids.end()) {
+            std::vector<PathComponent> pc;
+            if (!split_selector(sel, &pc)) {
+                p.state = P_UNSUPPORTED;
+                out->pattern_status[i] = AUTHJX_PAT_UNSUPPORTED;
+                out->pattern_error[i] = "selector syntax not compiled for the device";
+                flags |= 2;
+                continue;
+            }
+            Selector s;
+            s.comp_begin = (uint32_t)comps.size();
+            s.comp_count = (uint32_t)pc.size();
+            for (const PathComponent& c : pc) {
+                Component k;
+                k.lit_off = (uint32_t)lits.size();
+                k.lit_len = (uint32_t)c.key.size();
+                k.array_index = c.array_index;
+                k.hash = fnv1a(c.key);
+                lits += c.key;
+                comps.push_back(k);
+            }
+            it = sel_ids.emplace(sel, (uint32_t)sels.size()).first;
+            sels.push_back(s);
+        }
+        p.selector = it->second;
+    }
+
+    // ---- assemble ----
+    Builder b;
+    RulesetHdr hdr;
+    std::memset(&hdr, 0, sizeof hdr);
+    b.append(&hdr, sizeof hdr);
+    hdr.off_selectors = (uint32_t)b.align16();
+    b.append(sels.data(), sels.size() * sizeof(Selector));
+    hdr.off_components = (uint32_t)b.align16();
+    b.append(comps.data(), comps.size() * sizeof(Component));
+    hdr.off_code = (uint32_t)b.align16();
+    b.append(code.data(), code.size() * sizeof(uint32_t));
+    hdr.off_literals = (uint32_t)b.align16();
+    b.append(lits.data(), lits.size());
+    for (uint32_t i = 0; i < np; i++) {
+        if (dfa_of[i] < 0) continue;
+        const RegexDfa& d = dfas[(size_t)dfa_of[i]];
+        DfaHdr dh;
+        std::memset(&dh, 0, sizeof dh);
+        dh.n_states = d.n_states;
+        dh.n_classes = d.n_classes;
+        dh.start = d.start;
+        dh.match_state = d.match_state;
+        dh.n_ranges = (uint32_t)d.ranges.size();
+        std::memcpy(dh.ascii_class, d.ascii_class, 128);
+        size_t hoff = b.align16();
+        b.append(&dh, sizeof dh);
+        size_t toff = b.align16();
+        b.append(d.trans.data(), d.trans.size() * sizeof(uint16_t));
+        size_t eoff = b.align16();
+        b.append(d.eot.data(), d.eot.size());
+        size_t roff = b.align16();
+        b.append(d.ranges.data(), d.ranges.size() * sizeof(RuneRange));
+        DfaHdr* hp = reinterpret_cast<DfaHdr*>(b.blob.data() + hoff);
+        hp->trans_off = (uint32_t)toff;
+        hp->eot_off = (uint32_t)eoff;
+        hp->ranges_off = (uint32_t)roff;
+        pats[i].dfa_off = (uint32_t)hoff;
+    }
+    hdr.off_patterns = (uint32_t)b.align16();
+    b.append(pats.data(), pats.size() * sizeof(Pattern));
+    b.align16();
+    if (b.blob.size() > 0xFFFFFFFFull) return AUTHJX_ELIMIT;
+    hdr.magic = kMagic;
+    hdr.total_bytes = (uint32_t)b.blob.size();
+    hdr.n_patterns = np;
+    hdr.n_selectors = (uint32_t)sels.size();
+    hdr.n_code = (uint32_t)code.size();
+    hdr.max_depth = max_depth;
+    hdr.lit_bytes = (uint32_t)lits.size();
+    hdr.n_components = (uint32_t)comps.size();
+    hdr.flags = flags;
+    std::memcpy(b.blob.data(), &hdr, sizeof hdr);
+    out->blob = std::move(b.blob);
+    out->n_patterns = np;
+    out->n_selectors = (uint32_t)sels.size();
+    out->max_depth = max_depth;
+    return AUTHJX_OK;
+}
+
+}  // namespace ajx

@@ -1,0 +1,96 @@
+// ajx_kernels.hip — gfx950 kernels of the batched evaluator.
+//
+// ajx_eval_scan: one work-item per request (a wave evaluates 64 requests). For every
+// distinct selector of the request's ruleset it runs gj_get over the request's
+// document (the gjson scan), then evaluates every pattern on the resolved values
+// (Pattern.Matches), writes the per-pattern T bitmap and folds the And/Or tree into the
+// request's tri-state. Exact for arbitrary input bytes (well-formed or not).
+#include <hip/hip_runtime.h>
+
+#include "ajx_device.h"
+#include "ajx_kernels.h"
+
+namespace ajx {
+
+constexpr int kSelCache = 32;   // resolved selector values kept per request
+constexpr int kPatCache = 64;   // pattern results kept per request for the fold
+
+__global__ __launch_bounds__(256) void ajx_eval_scan(const uint8_t* const* __restrict__ sets,
+                                                     const uint32_t* __restrict__ set_of_req,
+                                                     const uint8_t* __restrict__ arena,
+                                                     const uint64_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ lens, uint32_t n,
+                                                     uint8_t* __restrict__ out_tri,
+                                                     int32_t* __restrict__ out_err,
+                                                     uint64_t* __restrict__ out_bm, uint32_t stride) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    const Selector* sels = reinterpret_cast<const Selector*>(blob + h->off_selectors);
+    const Component* comps = reinterpret_cast<const Component*>(blob + h->off_components);
+    const Pattern* pats = reinterpret_cast<const Pattern*>(blob + h->off_patterns);
+    const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
+    const uint8_t* lits = blob + h->off_literals;
+    const uint8_t* doc = arena + offs[r];
+    const uint32_t len = lens[r];
+
+    const uint32_t ns = h->n_selectors, np = h->n_patterns;
+    ValueRef vals[kSelCache];
+    const bool cache_sel = ns <= (uint32_t)kSelCache;
+    if (cache_sel)
+        for (uint32_t s = 0; s < ns; s++)
+            vals[s] = gj_get(doc, len, comps + sels[s].comp_begin, sels[s].comp_count, lits);
+
+    auto value_of = [&](uint32_t p) -> ValueRef {
+        const Selector& s = sels[pats[p].selector];
+        if (cache_sel) return vals[pats[p].selector];
+        return gj_get(doc, len, comps + s.comp_begin, s.comp_count, lits);
+    };
+    auto eval = [&](uint32_t p) -> uint8_t {
+        const Pattern& pt = pats[p];
+        if (pt.state != P_OK) return eval_pattern(blob, pt, doc, ValueRef{0, 0, T_NULL, 0});
+        return eval_pattern(blob, pt, doc, value_of(p));
+    };
+
+    uint8_t res[kPatCache];
+    const bool cache_pat = np <= (uint32_t)kPatCache;
+    if (out_bm) {
+        uint64_t* row = out_bm + (size_t)r * stride;
+        for (uint32_t w = 0; w < stride; w++) {
+            uint64_t word = 0;
+            for (uint32_t b = 0; b < 64; b++) {
+                uint32_t p = w * 64 + b;
+                if (p >= np) break;
+                uint8_t v = eval(p);
+                if (cache_pat) res[p] = v;
+                if (v == V_T) word |= 1ull << b;
+            }
+            row[w] = word;
+        }
+    }
+    int32_t ep;
+    uint8_t t;
+    if (cache_pat) {
+        if (!out_bm)
+            for (uint32_t p = 0; p < np; p++) res[p] = eval(p);
+        t = run_fold(code, h->n_code, [&](uint32_t p) { return res[p]; }, &ep);
+    } else {
+        t = run_fold(code, h->n_code, eval, &ep);
+    }
+    out_tri[r] = t;
+    if (out_err) out_err[r] = ep;
+}
+
+hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
+                            const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
+                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t block = 256;
+    const uint32_t grid = (n + block - 1) / block;
+    hipLaunchKernelGGL(ajx_eval_scan, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
+                       d_lens, n, d_tri, d_err, d_bm, stride);
+    return hipGetLastError();
+}
+
+}  // namespace ajx

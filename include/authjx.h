@@ -1,0 +1,151 @@
+/*
+ * authjx.h — C-ABI of libauthjx.so, the MI355X-native batched evaluator for Authorino's
+ * pattern-matching authorization hot path.
+ *
+ * Plain C types only (pointers, sizes, integers); no torch / HIP types in signatures
+ * (`stream` is an opaque hipStream_t passed as void*). All functions are reentrant;
+ * compiled rulesets are immutable after authjx_compile and may be shared by any number
+ * of threads (the reference shares expression trees across goroutines:
+ * pkg/service/auth.go:300 copies AuthConfig by value, sharing its trees).
+ *
+ * Interface each entry point replaces (reference = modassarrana89/authorino):
+ *   authjx_compile          controllers/auth_config_controller.go:805-852
+ *                           buildJSONExpression / buildJSONExpressionPattern(s): the
+ *                           reconcile-time construction of a jsonexp tree. Here the tree
+ *                           (flattened, see authjx_tree) is compiled once into
+ *                           device-resident tables (selector paths, literal pool,
+ *                           fold bytecode, regex DFAs).
+ *   authjx_free             pkg/auth/auth.go:30-33 AuthConfigCleaner.Clean (called from
+ *                           pkg/evaluators/config.go:42-68 before re-translate/delete).
+ *   authjx_eval_batch[_device]
+ *                           pkg/jsonexp/expressions.go:102-104 Expression.Matches(json)
+ *                           (Pattern.Matches :59-96, And :111-125, Or :136-154) for a
+ *                           micro-batch of Authorization-JSON documents; its callers are
+ *                           pkg/evaluators/authorization/json.go:19 (JSON rules) and
+ *                           pkg/service/auth_pipeline.go:382 (every `when` gate).
+ *   authjx_pattern_error    the static error a pattern yields (regexp.Compile's
+ *                           "error parsing regexp: ..." or expressions.go:94
+ *                           "unsupported operator for json authorization").
+ */
+#ifndef AUTHJX_H
+#define AUTHJX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AUTHJX_ABI_VERSION 1
+
+/* return codes */
+#define AUTHJX_OK 0
+#define AUTHJX_EINVAL (-1)
+#define AUTHJX_ENOMEM (-2)
+#define AUTHJX_EDEVICE (-3)
+#define AUTHJX_ELIMIT (-4)
+
+/* jsonexp.Operator (pkg/jsonexp/expressions.go:12-19) */
+#define AUTHJX_OP_UNKNOWN 0
+#define AUTHJX_OP_EQ 1
+#define AUTHJX_OP_NEQ 2
+#define AUTHJX_OP_INCL 3
+#define AUTHJX_OP_EXCL 4
+#define AUTHJX_OP_MATCHES 5
+
+/* tree node kinds: jsonexp.Pattern, *jsonexp.And, *jsonexp.Or */
+#define AUTHJX_NODE_PATTERN 0
+#define AUTHJX_NODE_AND 1
+#define AUTHJX_NODE_OR 2
+
+/* Tri-state result of Expression.Matches: (false,nil)=F, (true,nil)=T, (false,err)=E.
+ * UNDECIDED: the device met a value it does not format exactly (a number with more
+ * than 15 significant digits / outside the normal range, a hex or underscore number
+ * literal); the caller must not take a decision from it. Never produced for
+ * documents made by Go's encoding/json with integer or <=15-digit numbers. */
+#define AUTHJX_F 0
+#define AUTHJX_T 1
+#define AUTHJX_E 2
+#define AUTHJX_UNDECIDED 3
+
+/* per-pattern compile status */
+#define AUTHJX_PAT_OK 0
+#define AUTHJX_PAT_STATIC_ERROR 1 /* Matches always returns (false, err): bad regex / op */
+#define AUTHJX_PAT_UNSUPPORTED 2  /* selector / regex syntax not compiled for the device */
+
+typedef struct authjx_ctx authjx_ctx;
+typedef struct authjx_ruleset authjx_ruleset;
+
+typedef struct {
+    const char* selector; /* gjson path (jsonexp.Pattern.Selector) */
+    uint32_t selector_len;
+    int32_t op; /* AUTHJX_OP_* */
+    const char* value; /* jsonexp.Pattern.Value */
+    uint32_t value_len;
+} authjx_pattern;
+
+typedef struct {
+    int32_t kind;  /* AUTHJX_NODE_* */
+    int32_t left;  /* node index or -1 (nil) */
+    int32_t right; /* node index or -1 (nil) */
+    int32_t pattern; /* pattern index for AUTHJX_NODE_PATTERN */
+} authjx_node;
+
+/* One jsonexp.Expression, flattened. root = -1 means a nil Expression. */
+typedef struct {
+    const authjx_pattern* patterns;
+    uint32_t n_patterns;
+    const authjx_node* nodes;
+    uint32_t n_nodes;
+    int32_t root;
+} authjx_tree;
+
+/* Device context: one per GPU (device ordinal). */
+int authjx_init(int device, authjx_ctx** out);
+void authjx_shutdown(authjx_ctx* ctx);
+int authjx_device_count(void);
+
+/* Compile one tree into a device-resident ruleset. pattern_status (n_patterns entries,
+ * may be NULL) receives AUTHJX_PAT_*. A ruleset that contains UNSUPPORTED patterns is
+ * still created; evaluating it yields AUTHJX_UNDECIDED for requests whose result
+ * depends on them. errbuf (may be NULL) receives a diagnostic. */
+int authjx_compile(authjx_ctx* ctx, const authjx_tree* tree, authjx_ruleset** out,
+                   int32_t* pattern_status, char* errbuf, size_t errcap);
+void authjx_free(authjx_ruleset* rs);
+uint32_t authjx_ruleset_patterns(const authjx_ruleset* rs);
+uint32_t authjx_ruleset_selectors(const authjx_ruleset* rs);
+/* Copies the static error text of pattern i ("" when it has none); returns its length. */
+size_t authjx_pattern_error(const authjx_ruleset* rs, uint32_t i, char* buf, size_t cap);
+
+/* Evaluate a batch whose documents are already in device memory (HBM).
+ *   sets[n_sets]      rulesets; request r uses sets[set_of_req ? set_of_req[r] : 0]
+ *   d_set_of_req      device u32[n] or NULL
+ *   d_arena           device bytes; document r = d_arena[d_offs[r] .. + d_lens[r])
+ *   d_out_tristate    device u8[n]  (AUTHJX_F/T/E/UNDECIDED)
+ *   d_out_err_idx     device i32[n] pattern whose error decided an E, else -1 (may be NULL)
+ *   d_out_bitmap      device u64[n * bitmap_stride_words]: bit p = pattern p evaluated to T
+ *                     (every pattern evaluated, no short-circuit), may be NULL
+ *   stream            hipStream_t (NULL = the context's stream). Asynchronous. */
+int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                             const uint32_t* d_set_of_req, const uint8_t* d_arena,
+                             const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                             uint8_t* d_out_tristate, int32_t* d_out_err_idx,
+                             uint64_t* d_out_bitmap, uint32_t bitmap_stride_words, void* stream);
+
+/* Same, from host buffers: copies to the device, evaluates, copies back; synchronous.
+ * This is the entry point a cgo shim's micro-batcher calls. */
+int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                      const uint32_t* set_of_req, const uint8_t* arena, uint64_t arena_len,
+                      const uint64_t* offs, const uint32_t* lens, uint32_t n,
+                      uint8_t* out_tristate, int32_t* out_err_idx, uint64_t* out_bitmap,
+                      uint32_t bitmap_stride_words);
+
+/* Kernel-only timing of the last authjx_eval_batch_device on the context stream,
+ * measured with HIP events around the dominant kernel (ms). */
+float authjx_last_kernel_ms(authjx_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,136 @@
+"""TEST-ONLY ctypes binding of tests/native/libajx_hosttest.so (host build of the kernels'
+per-document logic, for CPU-side debugging against the oracle). Not product code."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_NATIVE = os.path.join(_HERE, "native")
+_L = None
+
+
+class _Pattern(C.Structure):
+    _fields_ = [("selector", C.c_char_p), ("selector_len", C.c_uint32), ("op", C.c_int32),
+                ("value", C.c_char_p), ("value_len", C.c_uint32)]
+
+
+class _Node(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("left", C.c_int32), ("right", C.c_int32), ("pattern", C.c_int32)]
+
+
+class _Tree(C.Structure):
+    _fields_ = [("patterns", C.POINTER(_Pattern)), ("n_patterns", C.c_uint32),
+                ("nodes", C.POINTER(_Node)), ("n_nodes", C.c_uint32), ("root", C.c_int32)]
+
+
+def lib():
+    global _L
+    if _L is None:
+        subprocess.run(["make", "-s", "-C", _NATIVE], check=True)
+        L = C.CDLL(os.path.join(_NATIVE, "libajx_hosttest.so"))
+        L.ht_compile.argtypes = [C.POINTER(_Tree), C.POINTER(C.c_int32), C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
+        L.ht_compile.restype = C.c_void_p
+        L.ht_free.argtypes = [C.c_void_p]
+        L.ht_eval.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
+        L.ht_eval.restype = C.c_int
+        L.ht_get.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.ht_get.restype = C.c_int
+        L.ht_string.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32]
+        L.ht_string.restype = C.c_int
+        L.ht_regex.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
+        L.ht_regex.restype = C.c_void_p
+        L.ht_regex_free.argtypes = [C.c_void_p]
+        L.ht_regex_states.argtypes = [C.c_void_p]
+        L.ht_regex_states.restype = C.c_uint32
+        L.ht_regex_match.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32]
+        L.ht_regex_match.restype = C.c_int
+        _L = L
+    return _L
+
+
+def _b(s):
+    return s if isinstance(s, bytes) else s.encode("utf-8")
+
+
+def make_tree(patterns, nodes, root):
+    keep = []
+    parr = (_Pattern * max(len(patterns), 1))()
+    for i, (sel, op, val) in enumerate(patterns):
+        sb, vb = _b(sel), _b(val)
+        keep += [sb, vb]
+        parr[i] = _Pattern(sb, len(sb), int(op), vb, len(vb))
+    narr = (_Node * max(len(nodes), 1))()
+    for i, nd in enumerate(nodes):
+        narr[i] = _Node(*nd)
+    keep += [parr, narr]
+    t = _Tree(parr, len(patterns), narr, len(nodes), root)
+    return t, keep
+
+
+class HostRuleset:
+    def __init__(self, patterns, nodes, root):
+        self.n = len(patterns)
+        t, self._keep = make_tree(patterns, nodes, root)
+        st = (C.c_int32 * max(self.n, 1))()
+        err = C.create_string_buffer(512)
+        rc = C.c_int(0)
+        self._h = lib().ht_compile(C.byref(t), st, err, 512, C.byref(rc))
+        self.rc = rc.value
+        self.status = list(st)[: self.n]
+        self.error = err.value.decode()
+
+    @classmethod
+    def from_expression(cls, expr):
+        pats, nodes, root = expr.flatten()
+        return cls([(p.selector, int(p.operator), p.value) for p in pats], nodes, root)
+
+    def eval(self, doc):
+        d = _b(doc)
+        res = (C.c_uint8 * max(self.n, 1))()
+        err = C.c_int32(-1)
+        t = lib().ht_eval(self._h, d, len(d), res, C.byref(err))
+        return t, err.value, list(res)[: self.n]
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ht_free(self._h)
+
+
+def get(doc, path):
+    d, p = _b(doc), _b(path)
+    s, e = C.c_uint32(), C.c_uint32()
+    t = lib().ht_get(p, len(p), d, len(d), C.byref(s), C.byref(e))
+    return t, d[s.value:e.value] if t >= 0 else b""
+
+
+def string(doc, path):
+    d, p = _b(doc), _b(path)
+    buf = C.create_string_buffer(1 << 16)
+    k = lib().ht_string(p, len(p), d, len(d), buf, 1 << 16)
+    if k < 0:
+        return k
+    return buf.raw[:k]
+
+
+class HostRegex:
+    def __init__(self, pat):
+        p = _b(pat)
+        st = C.c_int()
+        err = C.create_string_buffer(512)
+        self._h = lib().ht_regex(p, len(p), C.byref(st), err, 512)
+        self.status = st.value
+        self.error = err.value.decode("utf-8", "replace")
+
+    def match(self, s):
+        s = _b(s)
+        return bool(lib().ht_regex_match(self._h, s, len(s)))
+
+    @property
+    def states(self):
+        return lib().ht_regex_states(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ht_regex_free(self._h)

@@ -1,0 +1,124 @@
+// host_eval.cpp — TEST-ONLY harness. Compiles the kernels' per-document logic
+// (authorino_amd/csrc/ajx_device.h) and the reconcile-time compiler for the host CPU so
+// the CPU test suite can check them against the oracle without a GPU. It is not part
+// of libauthjx.so and is never used by the product path (which has no CPU fallback).
+#define AJX_HD inline
+#include <cstring>
+#include <string>
+
+#include "../../authorino_amd/csrc/ajx_compiler.h"
+#include "../../authorino_amd/csrc/ajx_device.h"
+#include "../../authorino_amd/csrc/ajx_regex.h"
+
+using namespace ajx;
+
+struct HtRuleset {
+    CompiledRuleset c;
+};
+
+extern "C" {
+
+void* ht_compile(const authjx_tree* tree, int32_t* status, char* err, size_t cap, int* rc) {
+    HtRuleset* r = new HtRuleset();
+    std::string e;
+    *rc = compile_tree(tree, &r->c, &e);
+    if (err && cap) std::snprintf(err, cap, "%s", e.c_str());
+    if (*rc != AUTHJX_OK) { delete r; return nullptr; }
+    if (status)
+        for (uint32_t i = 0; i < r->c.n_patterns; i++) status[i] = r->c.pattern_status[i];
+    return r;
+}
+
+void ht_free(void* h) { delete (HtRuleset*)h; }
+
+// evaluate one document; res[p] receives each pattern's tri-state
+int ht_eval(void* h, const uint8_t* doc, uint32_t len, uint8_t* res, int32_t* err) {
+    const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
+    const RulesetHdr* hd = (const RulesetHdr*)blob;
+    const Selector* sels = (const Selector*)(blob + hd->off_selectors);
+    const Component* comps = (const Component*)(blob + hd->off_components);
+    const Pattern* pats = (const Pattern*)(blob + hd->off_patterns);
+    const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
+    const uint8_t* lits = blob + hd->off_literals;
+    for (uint32_t p = 0; p < hd->n_patterns; p++) {
+        ValueRef v{0, 0, T_NULL, 0};
+        if (pats[p].state == P_OK) {
+            const Selector& s = sels[pats[p].selector];
+            v = gj_get(doc, len, comps + s.comp_begin, s.comp_count, lits);
+        }
+        res[p] = eval_pattern(blob, pats[p], doc, v);
+    }
+    return run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
+}
+
+// value resolution only: type + raw span
+int ht_get(const char* path, uint32_t plen, const uint8_t* doc, uint32_t len, uint32_t* start, uint32_t* end) {
+    std::vector<PathComponent> pc;
+    if (!split_selector(std::string(path, plen), &pc)) return -1;
+    std::string lits;
+    std::vector<Component> comps;
+    for (auto& c : pc) {
+        Component k{(uint32_t)lits.size(), (uint32_t)c.key.size(), c.array_index, 0};
+        lits += c.key;
+        comps.push_back(k);
+    }
+    ValueRef v = gj_get(doc, len, comps.data(), (uint32_t)comps.size(), (const uint8_t*)lits.data());
+    *start = v.start;
+    *end = v.end;
+    return v.type;
+}
+
+// Result.String() of the value at path; returns length or -1 undecided / -2 unsupported
+int ht_string(const char* path, uint32_t plen, const uint8_t* doc, uint32_t len, uint8_t* out, uint32_t cap) {
+    std::vector<PathComponent> pc;
+    if (!split_selector(std::string(path, plen), &pc)) return -2;
+    std::string lits;
+    std::vector<Component> comps;
+    for (auto& c : pc) {
+        Component k{(uint32_t)lits.size(), (uint32_t)c.key.size(), c.array_index, 0};
+        lits += c.key;
+        comps.push_back(k);
+    }
+    ValueRef v = gj_get(doc, len, comps.data(), (uint32_t)comps.size(), (const uint8_t*)lits.data());
+    StrSrc s;
+    if (!string_of(doc, v, &s)) return -1;
+    uint32_t k = 0;
+    for (int c; (c = s.next()) >= 0;)
+        if (k < cap) out[k++] = (uint8_t)c;
+    return (int)k;
+}
+
+// regex: compile + match (host copy of the device DFA walk)
+void* ht_regex(const char* pat, uint32_t n, int* status, char* err, size_t cap) {
+    RegexDfa* d = new RegexDfa();
+    std::string e;
+    *status = compile_go_regex(std::string(pat, n), d, &e);
+    if (err && cap) std::snprintf(err, cap, "%s", e.c_str());
+    if (*status != RX_OK) { delete d; return nullptr; }
+    return d;
+}
+void ht_regex_free(void* d) { delete (RegexDfa*)d; }
+uint32_t ht_regex_states(void* d) { return ((RegexDfa*)d)->n_states; }
+int ht_regex_match(void* dv, const uint8_t* s, uint32_t n) {
+    RegexDfa* d = (RegexDfa*)dv;
+    // lay the DFA out like the blob does
+    std::vector<uint8_t> blob(sizeof(DfaHdr));
+    DfaHdr h;
+    std::memset(&h, 0, sizeof h);
+    h.n_states = d->n_states; h.n_classes = d->n_classes; h.start = d->start; h.match_state = d->match_state;
+    std::memcpy(h.ascii_class, d->ascii_class, 128);
+    h.trans_off = (uint32_t)blob.size();
+    blob.insert(blob.end(), (uint8_t*)d->trans.data(), (uint8_t*)(d->trans.data() + d->trans.size()));
+    h.eot_off = (uint32_t)blob.size();
+    blob.insert(blob.end(), d->eot.begin(), d->eot.end());
+    while (blob.size() % 16) blob.push_back(0);
+    h.ranges_off = (uint32_t)blob.size();
+    h.n_ranges = (uint32_t)d->ranges.size();
+    blob.insert(blob.end(), (uint8_t*)d->ranges.data(), (uint8_t*)(d->ranges.data() + d->ranges.size()));
+    std::memcpy(blob.data(), &h, sizeof h);
+    StrSrc src;
+    src.init_raw(s, 0, n);
+    return dfa_match(blob.data(), 0, &src) ? 1 : 0;
+}
+
+}  // extern "C"
