@@ -749,6 +749,7 @@ Frag compile_node(Prog& p, const Node* n) {
                 tail = Frag{sp, g.out};
                 have_tail = true;
             }
+            if (!have_tail) return acc;  // x{n}: no optional copies
             if (!have) return tail;
             return concat2(p, acc, tail);
         }

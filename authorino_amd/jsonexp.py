@@ -106,8 +106,6 @@ class Expression:
 class Pattern(Expression):
     """jsonexp.Pattern{Selector, Operator, Value} (expressions.go:53-57)."""
 
-    __slots__ = ("selector", "operator", "value")
-
     def __init__(self, selector: str = "", operator: Operator | int | str = UnknownOperator, value: str = ""):
         self.selector = selector
         if isinstance(operator, str):
@@ -122,8 +120,6 @@ class Pattern(Expression):
 class And(Expression):
     """jsonexp.And{Left, Right} (expressions.go:106-125); nil sides are skipped."""
 
-    __slots__ = ("left", "right")
-
     def __init__(self, left: Optional[Expression] = None, right: Optional[Expression] = None):
         self.left = left
         self.right = right
@@ -134,8 +130,6 @@ class And(Expression):
 
 class Or(Expression):
     """jsonexp.Or{Left, Right} (expressions.go:131-154); nil sides are skipped."""
-
-    __slots__ = ("left", "right")
 
     def __init__(self, left: Optional[Expression] = None, right: Optional[Expression] = None):
         self.left = left

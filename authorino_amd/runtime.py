@@ -1,0 +1,269 @@
+"""authorino_amd.runtime — binding of libauthjx.so (include/authjx.h) for Python callers.
+
+PyTorch is only plumbing here: it allocates HBM buffers and supplies the stream; all
+evaluation happens in the HIP kernels behind the C-ABI. There is no CPU fallback: if
+the library or a GPU is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libauthjx.so")
+
+OP_UNKNOWN, OP_EQ, OP_NEQ, OP_INCL, OP_EXCL, OP_MATCHES = range(6)
+F, T, E, UNDECIDED = 0, 1, 2, 3
+PAT_OK, PAT_STATIC_ERROR, PAT_UNSUPPORTED = 0, 1, 2
+
+
+class AuthjxError(RuntimeError):
+    pass
+
+
+class _Pattern(C.Structure):
+    _fields_ = [("selector", C.c_char_p), ("selector_len", C.c_uint32), ("op", C.c_int32),
+                ("value", C.c_char_p), ("value_len", C.c_uint32)]
+
+
+class _Node(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("left", C.c_int32), ("right", C.c_int32), ("pattern", C.c_int32)]
+
+
+class _Tree(C.Structure):
+    _fields_ = [("patterns", C.POINTER(_Pattern)), ("n_patterns", C.c_uint32),
+                ("nodes", C.POINTER(_Node)), ("n_nodes", C.c_uint32), ("root", C.c_int32)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+EXPORTS = [
+    "authjx_init", "authjx_shutdown", "authjx_device_count", "authjx_compile", "authjx_free",
+    "authjx_ruleset_patterns", "authjx_ruleset_selectors", "authjx_pattern_error",
+    "authjx_eval_batch_device", "authjx_eval_batch", "authjx_last_kernel_ms",
+]
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libauthjx.so and declare its signatures (does not touch the GPU)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise AuthjxError(f"libauthjx.so not built at {path}: run __graft_entry__.build()")
+        L = C.CDLL(path)
+        L.authjx_init.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.authjx_init.restype = C.c_int
+        L.authjx_shutdown.argtypes = [C.c_void_p]
+        L.authjx_shutdown.restype = None
+        L.authjx_device_count.argtypes = []
+        L.authjx_device_count.restype = C.c_int
+        L.authjx_compile.argtypes = [C.c_void_p, C.POINTER(_Tree), C.POINTER(C.c_void_p), C.POINTER(C.c_int32),
+                                     C.c_char_p, C.c_size_t]
+        L.authjx_compile.restype = C.c_int
+        L.authjx_free.argtypes = [C.c_void_p]
+        L.authjx_free.restype = None
+        L.authjx_ruleset_patterns.argtypes = [C.c_void_p]
+        L.authjx_ruleset_patterns.restype = C.c_uint32
+        L.authjx_ruleset_selectors.argtypes = [C.c_void_p]
+        L.authjx_ruleset_selectors.restype = C.c_uint32
+        L.authjx_pattern_error.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]
+        L.authjx_pattern_error.restype = C.c_size_t
+        L.authjx_eval_batch_device.argtypes = [
+            C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+            C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
+        L.authjx_eval_batch_device.restype = C.c_int
+        L.authjx_eval_batch.argtypes = [
+            C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+            C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
+        L.authjx_eval_batch.restype = C.c_int
+        L.authjx_last_kernel_ms.argtypes = [C.c_void_p]
+        L.authjx_last_kernel_ms.restype = C.c_float
+        _lib = L
+        return L
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        names = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ELIMIT"}
+        raise AuthjxError(f"{what} failed: {names.get(rc, rc)}")
+
+
+def _b(s) -> bytes:
+    return s if isinstance(s, bytes) else s.encode("utf-8")
+
+
+class Context:
+    """One device context (HIP stream + set table) per GPU."""
+
+    def __init__(self, device: int = 0):
+        L = load_library()
+        if L.authjx_device_count() <= device:
+            raise AuthjxError(f"no HIP device {device} (authjx_device_count={L.authjx_device_count()})")
+        h = C.c_void_p()
+        _check(L.authjx_init(device, C.byref(h)), "authjx_init")
+        self._h = h
+        self.device = device
+
+    def compile(self, patterns: Sequence[Tuple[str, int, str]], nodes: Sequence[Tuple[int, int, int, int]],
+                root: int) -> "Ruleset":
+        return Ruleset(self, patterns, nodes, root)
+
+    def compile_expression(self, expr) -> "Ruleset":
+        pats, nodes, root = expr.flatten()
+        return Ruleset(self, [(p.selector, int(p.operator), p.value) for p in pats], nodes, root)
+
+    def eval_device(self, sets: Sequence["Ruleset"], arena, offs, lens, out_tri, out_err=None, out_bm=None,
+                    set_of_req=None, stream=None) -> None:
+        """Evaluate a batch resident in HBM (torch tensors on this device). Asynchronous."""
+        n = int(lens.numel())
+        words = int(out_bm.shape[1]) if out_bm is not None else 0
+        sarr = (C.c_void_p * len(sets))(*[s._h.value for s in sets])
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        rc = load_library().authjx_eval_batch_device(
+            self._h, sarr, len(sets), ptr(set_of_req), ptr(arena), ptr(offs), ptr(lens), n,
+            ptr(out_tri), ptr(out_err), ptr(out_bm), words, C.c_void_p(stream) if stream else None)
+        _check(rc, "authjx_eval_batch_device")
+
+    def last_kernel_ms(self) -> float:
+        return float(load_library().authjx_last_kernel_ms(self._h))
+
+    def eval_host(self, sets: Sequence["Ruleset"], docs: Sequence[bytes], set_of_req=None, with_bitmap=True):
+        """Evaluate host documents (copies to HBM and back); returns (tri, err, bitmap)."""
+        docs = [_b(d) for d in docs]
+        n = len(docs)
+        lens = np.fromiter((len(d) for d in docs), dtype=np.uint32, count=n)
+        offs = np.zeros(n, dtype=np.uint64)
+        if n:
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        arena = np.frombuffer(b"".join(docs) or b"\0", dtype=np.uint8)
+        return self.eval_host_arena(sets, arena, offs, lens, set_of_req, with_bitmap)
+
+    def eval_host_arena(self, sets, arena, offs, lens, set_of_req=None, with_bitmap=True):
+        n = int(lens.shape[0])
+        words = max(1, max((s.n_patterns + 63) // 64 for s in sets))
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        tri = np.zeros(max(n, 1), dtype=np.uint8)
+        err = np.zeros(max(n, 1), dtype=np.int32)
+        bm = np.zeros((max(n, 1), words), dtype=np.uint64) if with_bitmap else None
+        sor = None
+        if set_of_req is not None:
+            set_of_req = np.ascontiguousarray(set_of_req, dtype=np.uint32)
+            sor = C.c_void_p(set_of_req.ctypes.data)
+        sarr = (C.c_void_p * len(sets))(*[s._h.value for s in sets])
+        rc = load_library().authjx_eval_batch(
+            self._h, sarr, len(sets), sor, C.c_void_p(arena.ctypes.data), int(arena.nbytes),
+            C.c_void_p(offs.ctypes.data), C.c_void_p(lens.ctypes.data), n, C.c_void_p(tri.ctypes.data),
+            C.c_void_p(err.ctypes.data), C.c_void_p(bm.ctypes.data) if bm is not None else None,
+            words if bm is not None else 0)
+        _check(rc, "authjx_eval_batch")
+        return tri[:n], err[:n], (bm[:n] if bm is not None else None)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().authjx_shutdown(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Ruleset:
+    """A compiled jsonexp tree resident in HBM (authjx_compile / authjx_free)."""
+
+    def __init__(self, ctx: Context, patterns, nodes, root):
+        L = load_library()
+        self.ctx = ctx
+        self.n_patterns = len(patterns)
+        keep = []
+        parr = (_Pattern * max(len(patterns), 1))()
+        for i, (sel, op, val) in enumerate(patterns):
+            sb, vb = _b(sel), _b(val)
+            keep += [sb, vb]
+            parr[i] = _Pattern(sb, len(sb), int(op), vb, len(vb))
+        narr = (_Node * max(len(nodes), 1))()
+        for i, nd in enumerate(nodes):
+            narr[i] = _Node(*nd)
+        tree = _Tree(parr, len(patterns), narr, len(nodes), root)
+        st = (C.c_int32 * max(len(patterns), 1))()
+        err = C.create_string_buffer(512)
+        h = C.c_void_p()
+        rc = L.authjx_compile(ctx._h, C.byref(tree), C.byref(h), st, err, 512)
+        if rc != 0:
+            raise AuthjxError(f"authjx_compile failed ({rc}): {err.value.decode(errors='replace')}")
+        self._h = h
+        self.status = list(st)[: len(patterns)]
+        self.n_selectors = int(L.authjx_ruleset_selectors(h))
+
+    def pattern_error(self, i: int) -> str:
+        buf = C.create_string_buffer(1024)
+        load_library().authjx_pattern_error(self._h, i, buf, 1024)
+        return buf.value.decode("utf-8", "replace")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            try:
+                load_library().authjx_free(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+
+# -------------------------------------------------------------------------------------
+# jsonexp.Expression adapter
+# -------------------------------------------------------------------------------------
+_ctx_lock = threading.Lock()
+_default_ctx: Dict[int, Context] = {}
+
+
+def context(device: int = 0) -> Context:
+    with _ctx_lock:
+        if device not in _default_ctx:
+            _default_ctx[device] = Context(device)
+        return _default_ctx[device]
+
+
+class MatchError(Exception):
+    """The (false, err) result of Pattern.Matches: carries the Go error text."""
+
+
+class CompiledExpression:
+    def __init__(self, expr, device: int = 0):
+        self.ctx = context(device)
+        self.ruleset = self.ctx.compile_expression(expr)
+
+    def _to_result(self, t: int, ep: int):
+        if t == T:
+            return True, None
+        if t == F:
+            return False, None
+        if t == E:
+            return False, MatchError(self.ruleset.pattern_error(ep))
+        raise AuthjxError("device could not decide this document (AUTHJX_UNDECIDED)")
+
+    def matches(self, json):
+        tri, err, _ = self.ctx.eval_host([self.ruleset], [_b(json)], with_bitmap=False)
+        return self._to_result(int(tri[0]), int(err[0]))
+
+    def matches_batch(self, docs):
+        tri, err, _ = self.ctx.eval_host([self.ruleset], [_b(d) for d in docs], with_bitmap=False)
+        return [self._to_result(int(t), int(e)) for t, e in zip(tri, err)]
+
+
+def expression_for(expr) -> CompiledExpression:
+    c = getattr(expr, "_compiled", None)
+    if c is None:
+        c = CompiledExpression(expr)
+        expr._compiled = c
+    return c

@@ -1,0 +1,258 @@
+"""Synthetic Authorization-JSON workloads for the BASELINE.json configs.
+
+Documents follow the shape pkg/service/auth_pipeline.go:542-616 produces with Go's
+encoding/json (compact, map keys sorted, `<>&` escaped as \\u003c \\u003e \\u0026):
+  {"context":{"request":{"http":{...headers...}}},"request":{...},"source":{...},
+   "destination":{...},"auth":{"identity":{...JWT claims...},"metadata":{...}}}
+No dataset is fetched: everything is generated from numpy default_rng(seed).
+
+  c1  1 doc, All(eq auth.identity.sub, incl auth.identity.groups, matches path)
+  c2  N docs of 768..1280 B, one All of 16 eq/neq/incl patterns over 12 selectors
+  c3  N docs, 64 patterns (24 eq, 12 neq, 10 incl, 10 excl, 8 matches),
+      All(Any x4 of 8, All x4 of 8)
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from .jsonexp import (All, Any, EqualOperator, ExcludesOperator, IncludesOperator, NotEqualOperator, Pattern,
+                      RegexOperator)
+
+_GO_ESC = {"<": "\\u003c", ">": "\\u003e", "&": "\\u0026", " ": "\\u2028", " ": "\\u2029"}
+
+
+def go_json(obj) -> str:
+    """encoding/json.Marshal: compact, HTML-safe escapes (the form GetAuthorizationJSON
+    hands to Matches). Dict insertion order stands for Go struct field order; callers
+    pass Go maps through go_map() so their keys come out sorted like Go's."""
+    s = json.dumps(obj, separators=(",", ":"), ensure_ascii=False)
+    for k, v in _GO_ESC.items():
+        s = s.replace(k, v)
+    return s
+
+
+@dataclass
+class Workload:
+    name: str
+    arena: np.ndarray  # uint8
+    offs: np.ndarray   # uint64
+    lens: np.ndarray   # uint32
+    expr: object       # jsonexp.Expression
+    description: str
+
+    @property
+    def n(self) -> int:
+        return int(self.lens.shape[0])
+
+    @property
+    def n_patterns(self) -> int:
+        return len(self.expr.flatten()[0])
+
+    def doc(self, i: int) -> bytes:
+        o = int(self.offs[i])
+        return self.arena[o:o + int(self.lens[i])].tobytes()
+
+
+METHODS = ["GET"] * 19 + ["POST"]
+HEADER_NAMES = ["accept", "accept-encoding", "accept-language", "cache-control", "content-type", "cookie",
+                "origin", "referer", "user-agent", "x-b3-spanid", "x-b3-traceid", "x-envoy-attempt-count",
+                "x-forwarded-for", "x-forwarded-proto", "x-request-id", "x-amzn-trace-id", "x-client-version",
+                "x-correlation-id", "x-device-id", "x-session", "sec-fetch-mode", "sec-fetch-site", "pragma",
+                "dnt"]
+GROUPS = ["users", "admins", "devs", "ops", "billing", "support", "qa", "sales"]
+ROLES = ["reader", "writer", "auditor", "owner", "viewer", "editor"]
+
+
+def go_map(d: dict) -> dict:
+    """A Go map: encoding/json writes its keys sorted."""
+    return {k: d[k] for k in sorted(d)}
+
+
+def _hex(rng, k):
+    return "".join(rng.choice(list("0123456789abcdef"), size=k))
+
+
+def _make_doc(rng: np.random.Generator, target_len: int, uid: int) -> bytes:
+    p = rng.random(16)
+    method = "GET" if p[0] < 0.95 else rng.choice(["POST", "PUT", "DELETE"])
+    sub = "user-%04d" % (uid % 10000) if p[1] < 0.95 else "user-0000"
+    headers = {}
+    for name in rng.choice(HEADER_NAMES, size=int(rng.integers(3, 9)), replace=False):
+        headers[str(name)] = _hex(rng, int(rng.integers(4, 16)))
+    headers["x-tenant"] = "acme" if p[2] < 0.95 else "globex"
+    if p[3] >= 0.95:
+        headers["x-blocked"] = "1"
+    headers["authorization"] = "Bearer " + _hex(rng, 16)
+    headers["user-agent"] = "Mozilla/5.0 (X11; Linux x86_64) curl/8.%d & friends <bot>" % int(rng.integers(0, 9))
+    headers[":path"] = "/api/v%d/orders/%d" % (int(rng.integers(1, 4)), int(rng.integers(1, 100000)))
+    host = "api.example.com" if p[4] < 0.95 else "api.example.org"
+    path = headers[":path"] if p[5] < 0.95 else "/admin/metrics"
+    groups = [g for g in GROUPS if rng.random() < 0.3]
+    if p[6] < 0.95:
+        groups.append("users")
+    if p[7] < 0.05:
+        groups.append("banned")
+    roles = [r for r in ROLES if rng.random() < 0.3]
+    if p[8] < 0.95:
+        roles.append("reader")
+    http = {"id": str(int(rng.integers(10**15, 10**16))), "method": str(method), "headers": go_map(headers),
+            "path": path, "host": host, "scheme": "https" if p[9] < 0.95 else "http", "protocol": "HTTP/1.1"}
+    identity = go_map({
+        "aud": "talker-api" if p[10] < 0.95 else "other-api",
+        "azp": "talker-api", "email": "%s@%s" % (sub, "example.com" if p[11] < 0.95 else "evil.io"),
+        "email_verified": bool(p[12] < 0.95), "exp": int(1700000000 + rng.integers(0, 10**6)),
+        "groups": sorted(set(groups)), "iat": int(1699990000 + rng.integers(0, 10**6)),
+        "iss": "https://sso.example.com/realms/acme" if p[13] < 0.95 else "https://sso.evil.io/realms/x",
+        "name": "User %d" % uid, "preferred_username": sub,
+        "realm_access": {"roles": sorted(set(roles))}, "scope": "openid email profile",
+        "sub": sub, "typ": "Bearer", "acr": 0.5,
+    })
+    doc = {
+        "context": {"source": {"address": {"socketAddress": {"address": "10.%d.%d.%d" % tuple(rng.integers(0, 255, 3)),
+                                                              "portValue": int(rng.integers(1024, 65535))}}},
+                    "request": {"time": {"seconds": int(1700000000 + uid)}, "http": http}},
+        "request": {"host": host, "method": str(method), "path": path, "url_path": path.split("?")[0],
+                    "headers": go_map({"authorization": headers["authorization"]})},
+        "source": {"address": "10.0.0.%d" % int(rng.integers(1, 250)) if p[14] < 0.95 else "10.66.6.6"},
+        "destination": {"address": "10.1.0.1", "port": 8080},
+        "auth": {"identity": identity, "metadata": go_map({"tenant": {"plan": "gold" if p[15] < 0.95 else "free"}})},
+    }
+    s = go_json(doc)
+    # pad (a header value) to the target length
+    short = target_len - len(s)
+    if short > 20:
+        headers["x-padding"] = "p" * (short - len(',"x-padding":""'))
+        http["headers"] = go_map(headers)
+        s = go_json(doc)
+    return s.encode("utf-8")
+
+
+def make_docs(n: int, seed: int, lo: int = 768, hi: int = 1280, unique: int = 4096) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """n documents (lengths ~U[lo, hi]) packed into (arena, offs, lens). `unique` distinct
+    documents are generated and tiled by a random permutation."""
+    rng = np.random.default_rng(seed)
+    m = min(n, unique)
+    base = [_make_doc(rng, int(rng.integers(lo, hi + 1)), i) for i in range(m)]
+    idx = rng.integers(0, m, size=n) if n > m else np.arange(n)
+    parts = [base[i] for i in idx]
+    lens = np.fromiter((len(b) for b in parts), dtype=np.uint32, count=n)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    arena = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    return arena, offs, lens
+
+
+def c1_expression():
+    return All(
+        Pattern("auth.identity.sub", EqualOperator, "user-0042"),
+        Pattern("auth.identity.groups", IncludesOperator, "admins"),
+        Pattern("context.request.http.path", RegexOperator, r"^/api/v[0-9]+/orders/[0-9]+$"),
+    )
+
+
+def c2_expression():
+    """16 patterns (8 eq, 4 neq, 4 incl) over 12 distinct selectors, each true w.p. ~0.95."""
+    return All(
+        Pattern("context.request.http.method", EqualOperator, "GET"),
+        Pattern("context.request.http.host", EqualOperator, "api.example.com"),
+        Pattern("context.request.http.scheme", EqualOperator, "https"),
+        Pattern("context.request.http.headers.x-tenant", EqualOperator, "acme"),
+        Pattern("auth.identity.iss", EqualOperator, "https://sso.example.com/realms/acme"),
+        Pattern("auth.identity.aud", EqualOperator, "talker-api"),
+        Pattern("auth.identity.email_verified", EqualOperator, "true"),
+        Pattern("auth.metadata.tenant.plan", EqualOperator, "gold"),
+        Pattern("context.request.http.headers.x-blocked", NotEqualOperator, "1"),
+        Pattern("auth.identity.sub", NotEqualOperator, "user-0000"),
+        Pattern("context.request.http.method", NotEqualOperator, "DELETE"),
+        Pattern("source.address", NotEqualOperator, "10.66.6.6"),
+        Pattern("auth.identity.groups", IncludesOperator, "users"),
+        Pattern("auth.identity.realm_access.roles", IncludesOperator, "reader"),
+        Pattern("auth.identity.groups", IncludesOperator, "users"),
+        Pattern("auth.identity.realm_access.roles", IncludesOperator, "reader"),
+    )
+
+
+def c3_expression():
+    """64 patterns: 24 eq, 12 neq, 10 incl, 10 excl, 8 matches; All(Any x4 of 8, All x4 of 8)."""
+    eq = [
+        ("context.request.http.method", "GET"), ("context.request.http.host", "api.example.com"),
+        ("context.request.http.scheme", "https"), ("context.request.http.headers.x-tenant", "acme"),
+        ("auth.identity.iss", "https://sso.example.com/realms/acme"), ("auth.identity.aud", "talker-api"),
+        ("auth.identity.email_verified", "true"), ("auth.metadata.tenant.plan", "gold"),
+        ("request.method", "GET"), ("request.host", "api.example.com"), ("auth.identity.typ", "Bearer"),
+        ("auth.identity.azp", "talker-api"), ("context.request.http.protocol", "HTTP/1.1"),
+        ("destination.port", "8080"), ("auth.identity.acr", "0.5"), ("destination.address", "10.1.0.1"),
+        ("auth.identity.scope", "openid email profile"), ("request.url_path", "/admin/metrics"),
+        ("context.request.http.headers.x-blocked", "1"), ("auth.identity.sub", "user-0042"),
+        ("auth.identity.realm_access.roles.0", "auditor"), ("auth.identity.groups.0", "admins"),
+        ("context.request.http.headers.content-type", "application/json"), ("auth.identity.name", "User 42"),
+    ]
+    neq = [
+        ("context.request.http.headers.x-blocked", "1"), ("auth.identity.sub", "user-0000"),
+        ("context.request.http.method", "DELETE"), ("source.address", "10.66.6.6"),
+        ("auth.identity.aud", "other-api"), ("auth.metadata.tenant.plan", "free"),
+        ("context.request.http.scheme", "http"), ("request.host", "api.example.org"),
+        ("auth.identity.iss", "https://sso.evil.io/realms/x"), ("context.request.http.headers.x-tenant", "globex"),
+        ("auth.identity.email_verified", "false"), ("request.method", "PUT"),
+    ]
+    incl = [("auth.identity.groups", "users"), ("auth.identity.realm_access.roles", "reader"),
+            ("auth.identity.groups", "admins"), ("auth.identity.realm_access.roles", "owner"),
+            ("auth.identity.groups", "devs"), ("auth.identity.realm_access.roles", "writer"),
+            ("auth.identity.groups", "ops"), ("auth.identity.realm_access.roles", "viewer"),
+            ("auth.identity.groups", "qa"), ("auth.identity.aud", "talker-api")]
+    excl = [("auth.identity.groups", "banned"), ("auth.identity.realm_access.roles", "root"),
+            ("auth.identity.groups", "sales"), ("auth.identity.realm_access.roles", "editor"),
+            ("auth.identity.groups", "billing"), ("auth.identity.groups", "support"),
+            ("auth.identity.realm_access.roles", "auditor"), ("auth.identity.groups", "guests"),
+            ("auth.identity.realm_access.roles", "nobody"), ("auth.identity.sub", "user-0000")]
+    rx = [
+        ("context.request.http.path", r"^/api/v[0-9]+/orders/[0-9]+$"),
+        ("context.request.http.method", r"^(GET|HEAD|OPTIONS)$"),
+        ("auth.identity.email", r"@example\.com$"),
+        ("context.request.http.headers.user-agent", r"(?i)mozilla/5\.0 .*curl/\d+"),
+        ("auth.identity.iss", r"^https://sso\.[a-z]+\.com/realms/[a-z]+$"),
+        ("context.request.http.headers.x-request-id", r"^[0-9a-f]{4,16}$"),
+        ("request.url_path", r"^/admin(/.*)?$"),
+        ("auth.identity.preferred_username", r"^user-\d{4}$"),
+    ]
+    likely_eq, rare_eq = eq[:17], eq[17:]
+    likely_incl, med_incl = [incl[0], incl[1], incl[9]], incl[2:9]
+    likely_excl, med_excl = [excl[0], excl[1], excl[7], excl[8], excl[9]], excl[2:7]
+    likely_rx, med_rx = [rx[0], rx[1], rx[2], rx[3], rx[4], rx[7]], [rx[5], rx[6]]
+    likely = ([Pattern(s, EqualOperator, v) for s, v in likely_eq] + [Pattern(s, NotEqualOperator, v) for s, v in neq]
+              + [Pattern(s, IncludesOperator, v) for s, v in likely_incl]
+              + [Pattern(s, ExcludesOperator, v) for s, v in likely_excl]
+              + [Pattern(s, RegexOperator, v) for s, v in likely_rx])
+    other = ([Pattern(s, EqualOperator, v) for s, v in rare_eq] + [Pattern(s, IncludesOperator, v) for s, v in med_incl]
+             + [Pattern(s, ExcludesOperator, v) for s, v in med_excl] + [Pattern(s, RegexOperator, v) for s, v in med_rx])
+    rng = np.random.default_rng(33)
+    likely = [likely[i] for i in rng.permutation(len(likely))]
+    all_pats, spare = likely[:32], likely[32:]
+    any_pats = spare + other
+    any_pats = [any_pats[i] for i in rng.permutation(len(any_pats))]
+    all_groups = [all_pats[8 * k:8 * k + 8] for k in range(4)]
+    any_groups = [any_pats[8 * k:8 * k + 8] for k in range(4)]
+    return All(*[Any(*g) for g in any_groups], *[All(*g) for g in all_groups])
+
+
+def make(name: str, n: Optional[int] = None, seed: Optional[int] = None) -> Workload:
+    name = name.lower()
+    if name == "c1":
+        arena, offs, lens = make_docs(1, seed if seed is not None else 1, 680, 720)
+        return Workload("c1", arena, offs, lens, c1_expression(), "1 doc x All(eq, incl, matches)")
+    if name == "c2":
+        n = n if n is not None else 1 << 20
+        arena, offs, lens = make_docs(n, seed if seed is not None else 2)
+        return Workload("c2", arena, offs, lens, c2_expression(),
+                        f"{n} docs (768-1280 B) x All of 16 eq/neq/incl over 12 selectors")
+    if name == "c3":
+        n = n if n is not None else 1 << 20
+        arena, offs, lens = make_docs(n, seed if seed is not None else 3)
+        return Workload("c3", arena, offs, lens, c3_expression(),
+                        f"{n} docs x 64 patterns (24 eq/12 neq/10 incl/10 excl/8 matches), All(Any x4, All x4)")
+    raise ValueError(f"unknown workload {name!r}")

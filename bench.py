@@ -1,0 +1,193 @@
+"""bench.py — headline benchmark (BASELINE.json metric) for the pattern-matching hot path.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3] [--n N_REQUESTS]
+
+A step = one pass of the hot path (ajx kernels behind authjx_eval_batch_device) over one
+batch of N synthetic Authorization-JSON documents already resident in HBM. N=1 runs the
+config BASELINE.json's metric is quoted on that fits one GPU (configs[1], "c2": 1M
+requests x 16 eq/neq/incl patterns). Multi-GPU: one process per GPU
+(torch.distributed.run), each rank evaluates its own shard (weak scaling, no data-path
+collective); the timed region is bracketed by barrier + synchronize, the max over ranks
+is reported. Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2")
+    ap.add_argument("--n", type=int, default=1 << 20, help="requests per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(w, n_patterns, target_s, gpu_tri, gpu_bm):
+    """Oracle (C restatement, oracle/) on a bounded sample of the same workload; also the
+    parity check of the GPU results on that sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    pats, nodes, root = w.expr.flatten()
+    rs = pyoracle.Ruleset([(p.selector, int(p.operator), p.value) for p in pats], nodes, root)
+    pilot = min(w.n, 16384)
+    t0 = time.perf_counter()
+    pyoracle.eval_batch([rs], w.arena, w.offs[:pilot], w.lens[:pilot], nthreads=threads)
+    dt = max(time.perf_counter() - t0, 1e-6)
+    sample = int(min(w.n, max(pilot, pilot * target_s / dt)))
+    t0 = time.perf_counter()
+    tri, err, bm = pyoracle.eval_batch([rs], w.arena, w.offs[:sample], w.lens[:sample], nthreads=threads)
+    dt = time.perf_counter() - t0
+    mism = int((tri != gpu_tri[:sample]).sum()) + int((bm != gpu_bm[:sample]).any(axis=1).sum())
+    return {
+        "value": sample * n_patterns / dt,
+        "unit": "request×rule evals/s",
+        "decisions_per_s": sample / dt,
+        "cores": threads,
+        "kind": "port",
+        "sample": f"first {sample} of the {w.n} synthetic docs, same ruleset, oracle/ C restatement "
+                  f"(gjson re-scan per pattern like the reference), {threads} host threads, {dt:.1f}s",
+    }, {"sample": sample, "mismatches": mism}
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from authorino_amd import runtime, workloads
+
+    w = workloads.make(args.workload, n=args.n, seed=1000 + rank)
+    R = w.n_patterns
+    ctx = runtime.Context(local)
+    rs = ctx.compile_expression(w.expr)
+
+    arena = torch.from_numpy(w.arena).to(dev)
+    offs = torch.from_numpy(w.offs.view(np.int64)).to(dev)
+    lens = torch.from_numpy(w.lens.view(np.int32)).to(dev)
+    words = (R + 63) // 64
+    tri = torch.empty(w.n, dtype=torch.uint8, device=dev)
+    err = torch.empty(w.n, dtype=torch.int32, device=dev)
+    bm = torch.empty((w.n, words), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def step():
+        ctx.eval_device([rs], arena, offs, lens, tri, err, bm, stream=sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    total_req = w.n * args.steps * world
+    value = total_req * R / elapsed
+    algo_bytes = int(w.lens.astype(np.int64).sum()) + w.n * (math.ceil(R / 8) + 1)
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(args.pmc_json) as f:
+            pmc = json.load(f)
+        if pmc.get("workload") == args.workload and pmc.get("n") == w.n:
+            traffic = pmc.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    cpu, parity = None, None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu, parity = cpu_baseline(w, R, args.cpu_seconds, tri.cpu().numpy(), bm.cpu().numpy().view(np.uint64))
+    undecided = int((tri == runtime.UNDECIDED).sum().item())
+
+    if rank == 0:
+        line = {
+            "metric": "request×rule evals/sec (+ allow/deny decisions/sec, % HBM roofline)",
+            "value": value,
+            "unit": "request×rule evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "decisions_per_s": total_req / elapsed,
+            "config": {
+                "workload": args.workload,
+                "description": w.description,
+                "requests_per_gpu": w.n,
+                "patterns": R,
+                "selectors": rs.n_selectors,
+                "doc_bytes_mean": float(w.lens.mean()),
+                "parallelism": f"dp{world} (independent request shards, no collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "kernel_ms": kern_ms,
+                "algorithmic_bytes_per_launch": algo_bytes,
+            },
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "undecided": undecided,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

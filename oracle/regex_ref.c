@@ -948,6 +948,7 @@ static frag comp(or_regex* re, node* n) {
                 tail = q;
                 have_tail = 1;
             }
+            if (!have_tail) return acc; /* x{n}: no optional copies */
             if (!have) return tail;
             patch(re, &acc, tail.start);
             acc.out = tail.out;

@@ -1,0 +1,150 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the oracle.
+
+Bit-exact: per-request tri-state, per-pattern T bitmap and the deciding error pattern.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as O
+from kat_util import build, flat, load_kats
+
+pytestmark = pytest.mark.gpu
+
+KATS = load_kats()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from authorino_amd import runtime
+
+    return runtime.Context(0)
+
+
+def _oracle(w_expr, arena, offs, lens, set_of_req=None, sets=None):
+    if sets is None:
+        pats, nodes, root = flat(w_expr)
+        sets = [O.Ruleset(pats, nodes, root)]
+    return O.eval_batch(sets, arena, offs, lens, set_of_req=set_of_req, nthreads=8)
+
+
+def test_reference_kats_via_jsonexp_api():
+    """The jsonexp mirror (Expression.matches) on the reference's own vectors."""
+    for case in KATS:
+        expr = build(case["tree"])
+        ok, err = expr.matches(case["doc"])
+        if case["expect"] == "T":
+            assert ok and err is None, case
+        elif case["expect"] == "F":
+            assert not ok and err is None, case
+        else:
+            assert not ok and err is not None and case["error_contains"] in str(err), case
+
+
+def test_reference_kats_one_batch(ctx):
+    """All KATs in one multi-ruleset batch (set_of_req)."""
+    sets, osets, docs = [], [], []
+    for case in KATS:
+        pats, nodes, root = flat(build(case["tree"]))
+        sets.append(ctx.compile(pats, nodes, root))
+        osets.append(O.Ruleset(pats, nodes, root))
+        docs.append(case["doc"].encode())
+    sor = np.arange(len(KATS), dtype=np.uint32)
+    tri, err, bm = ctx.eval_host(sets, docs, set_of_req=sor)
+    lens = np.array([len(d) for d in docs], dtype=np.uint32)
+    offs = np.zeros(len(docs), dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1])
+    arena = np.frombuffer(b"".join(docs), dtype=np.uint8)
+    otri, oerr, obm = O.eval_batch(osets, arena, offs, lens, set_of_req=sor)
+    assert np.array_equal(tri, otri)
+    assert np.array_equal(err, oerr)
+    assert np.array_equal(bm, obm)
+
+
+@pytest.mark.parametrize("workload,n", [("c2", 50000), ("c3", 30000), ("c1", 1)])
+def test_workload_parity(ctx, workload, n):
+    from authorino_amd import workloads as W
+
+    w = W.make(workload, n=n)
+    rs = ctx.compile_expression(w.expr)
+    tri, err, bm = ctx.eval_host_arena([rs], w.arena, w.offs, w.lens)
+    otri, oerr, obm = _oracle(w.expr, w.arena, w.offs, w.lens)
+    assert np.array_equal(tri, otri)
+    assert np.array_equal(err, oerr)
+    assert np.array_equal(bm, obm)
+    assert (tri == 3).sum() == 0
+
+
+def test_full_size_c2_properties(ctx):
+    """BASELINE config c2 at full size (1M requests): bit-exact on a strided sample plus
+    size-independent properties (decision == AND of the 16 pattern bits for an All of
+    eq/neq/incl patterns; every pattern's T-rate near its design rate)."""
+    import torch
+
+    from authorino_amd import workloads as W
+
+    w = W.make("c2", n=1 << 20)
+    rs = ctx.compile_expression(w.expr)
+    dev = torch.device("cuda", 0)
+    arena = torch.from_numpy(w.arena).to(dev)
+    offs = torch.from_numpy(w.offs.view(np.int64)).to(dev)
+    lens = torch.from_numpy(w.lens.view(np.int32)).to(dev)
+    tri = torch.empty(w.n, dtype=torch.uint8, device=dev)
+    err = torch.empty(w.n, dtype=torch.int32, device=dev)
+    bm = torch.empty((w.n, 1), dtype=torch.int64, device=dev)
+    ctx.eval_device([rs], arena, offs, lens, tri, err, bm)
+    torch.cuda.synchronize()
+    tri = tri.cpu().numpy()
+    bits = bm.cpu().numpy().view(np.uint64)[:, 0]
+    allow = bits == np.uint64((1 << 16) - 1)
+    assert np.array_equal(tri == 1, allow)
+    assert set(np.unique(tri)) <= {0, 1}
+    rates = [((bits >> np.uint64(p)) & np.uint64(1)).mean() for p in range(16)]
+    assert min(rates) > 0.9
+    idx = np.arange(0, w.n, 97)
+    sub_offs, sub_lens = w.offs[idx], w.lens[idx]
+    otri, _, obm = _oracle(w.expr, w.arena, sub_offs, sub_lens)
+    assert np.array_equal(tri[idx], otri)
+    assert np.array_equal(bits[idx], obm[:, 0])
+
+
+def _mutations(rng, docs, k):
+    """Malformed / edge-case variants: truncation, byte flips, structural deletions."""
+    out = []
+    for _ in range(k):
+        d = bytearray(docs[int(rng.integers(0, len(docs)))])
+        m = int(rng.integers(0, 5))
+        if m == 0 and len(d) > 2:
+            d = d[: int(rng.integers(0, len(d)))]
+        elif m == 1 and len(d):
+            for _ in range(int(rng.integers(1, 4))):
+                d[int(rng.integers(0, len(d)))] = int(rng.choice(list(b'{}[]":,\\ 0a-eu')))
+        elif m == 2 and len(d) > 4:
+            i = int(rng.integers(0, len(d) - 1))
+            del d[i:i + int(rng.integers(1, 4))]
+        elif m == 3:
+            d = bytearray(b"  \n" + bytes(d) + b" trailing")
+        else:
+            d = bytearray(bytes(d).replace(b'"', b'\\"', 1))
+        out.append(bytes(d))
+    return out
+
+
+def test_malformed_and_edge_documents(ctx):
+    """Exact on arbitrary bytes: empty docs, truncated docs, flipped structural bytes."""
+    from authorino_amd import workloads as W
+
+    w = W.make("c3", n=400, seed=11)
+    base = [w.doc(i) for i in range(w.n)]
+    rng = np.random.default_rng(5)
+    docs = _mutations(rng, base, 4000) + [b"", b"{", b"[", b"{}", b"[]", b"null", b'"x"', b"{]", b"[}"]
+    rs = ctx.compile_expression(w.expr)
+    tri, err, bm = ctx.eval_host([rs], docs)
+    lens = np.array([len(d) for d in docs], dtype=np.uint32)
+    offs = np.zeros(len(docs), dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1])
+    arena = np.frombuffer(b"".join(docs) + b"\0", dtype=np.uint8)
+    otri, oerr, obm = _oracle(w.expr, arena, offs, lens)
+    dec = tri != 3
+    assert np.array_equal(tri[dec], otri[dec])
+    assert np.array_equal(bm[dec], obm[dec])
+    assert dec.mean() > 0.99
