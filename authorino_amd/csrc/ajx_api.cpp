@@ -32,6 +32,10 @@ struct authjx_ctx {
     // staging for authjx_eval_batch (host buffers)
     uint8_t* d_stage = nullptr;
     size_t stage_cap = 0;
+    // requests the fast kernel hands to the exact scan
+    uint32_t* d_slow = nullptr;  // [0] = count, [1..] = ids
+    uint32_t slow_cap = 0;
+    int force_scan = 0;
     float last_ms = 0.f;
 };
 
@@ -104,6 +108,7 @@ void authjx_shutdown(authjx_ctx* ctx) {
     if (ctx->d_sets) (void)hipFree(ctx->d_sets);
     if (ctx->h_sets_pinned) (void)hipHostFree(ctx->h_sets_pinned);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+    if (ctx->d_slow) (void)hipFree(ctx->d_slow);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -175,11 +180,43 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     HIP_OK(hipSetDevice(ctx->device));
     int rc = ensure_sets(ctx, sets, n_sets, s);
     if (rc != AUTHJX_OK) return rc;
+    if (!ctx->force_scan && n > ctx->slow_cap) {
+        // growing the list: no batch in flight on this context may still use it
+        HIP_OK(hipStreamSynchronize(s));
+        if (ctx->d_slow) (void)hipFree(ctx->d_slow);
+        ctx->d_slow = nullptr;
+        ctx->slow_cap = 0;
+        HIP_OK(hipMalloc(&ctx->d_slow, ((size_t)n + 1) * sizeof(uint32_t)));
+        ctx->slow_cap = n;
+    }
     HIP_OK(hipEventRecord(ctx->ev0, s));
-    HIP_OK(ajx::launch_eval_scan(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
-                                 d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
+    if (ctx->force_scan)
+        HIP_OK(ajx::launch_eval_scan(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
+                                     d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
+    else
+        HIP_OK(ajx::launch_eval_fast(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
+                                     d_out_err_idx, d_out_bitmap, bitmap_stride_words, ctx->d_slow, ctx->d_slow + 1,
+                                     s));
     HIP_OK(hipEventRecord(ctx->ev1, s));
     return AUTHJX_OK;
+}
+
+int authjx_set_exact_scan(authjx_ctx* ctx, int force) {
+    if (!ctx) return AUTHJX_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->force_scan = force ? 1 : 0;
+    return AUTHJX_OK;
+}
+
+int64_t authjx_last_exact_count(authjx_ctx* ctx) {
+    if (!ctx) return AUTHJX_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    if (ctx->force_scan || !ctx->d_slow) return -1;
+    uint32_t c = 0;
+    if (hipSetDevice(ctx->device) != hipSuccess || hipEventSynchronize(ctx->ev1) != hipSuccess ||
+        hipMemcpy(&c, ctx->d_slow, sizeof c, hipMemcpyDeviceToHost) != hipSuccess)
+        return AUTHJX_EDEVICE;
+    return (int64_t)c;
 }
 
 float authjx_last_kernel_ms(authjx_ctx* ctx) {

@@ -73,6 +73,38 @@ struct RuneRange {
     uint32_t lo, hi, cls, pad;
 };
 
+// ---- single-pass fast path: selector trie ---------------------------------------
+// All selectors of a ruleset merged into one trie over path components; node 0 is
+// the document root. A key (object context) or an element index (array context)
+// moves from a node to one of its children.
+constexpr uint32_t kFastMaxPatterns = 128;
+constexpr uint32_t kFastMaxNodes = 255;
+constexpr uint32_t kFastMaxSelectors = 64;
+constexpr uint8_t kNoNode = 0xFF;
+
+struct TrieNode {
+    uint16_t child_begin;  // index into TrieChild[]
+    uint8_t n_children;
+    uint8_t flags;         // bit0: has array-index children
+    int16_t selector;      // selector whose path ends here, -1 none
+    uint16_t pad;
+};
+
+struct TrieChild {
+    uint32_t prefix;       // first 4 key bytes, little-endian, zero padded
+    uint32_t key_len;
+    uint32_t key_off;      // key bytes in the literal pool
+    int32_t array_index;   // -1 never matches an element
+    uint32_t node;
+    uint32_t pad[3];
+};
+
+struct SelectorPatterns {
+    uint32_t begin;        // index into the uint16 pattern list
+    uint32_t count;
+    uint64_t mask[2];      // the same patterns as a bitmask
+};
+
 struct RulesetHdr {
     uint32_t magic;
     uint32_t total_bytes;
@@ -87,8 +119,17 @@ struct RulesetHdr {
     uint32_t off_literals;
     uint32_t lit_bytes;
     uint32_t n_components;
-    uint32_t flags;  // bit0: has regex; bit1: has unsupported pattern
-    uint32_t pad[2];
+    uint32_t flags;  // bit0: has regex; bit1: has unsupported pattern; bit2: fast path ok
+    uint32_t n_trie_nodes;
+    uint32_t off_trie_nodes;
+    uint32_t off_trie_children;
+    uint32_t off_sel_patterns;  // SelectorPatterns[n_selectors]
+    uint32_t off_pattern_lists; // uint16_t[]
+    uint32_t pad0;
+    uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
+    uint64_t static_error[2];   // pattern p is a static E
+    uint64_t unsupported[2];    // pattern p can not be decided on the device
 };
+constexpr uint32_t kFlagFastOk = 4;
 
 }  // namespace ajx

@@ -260,11 +260,114 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
         p.selector = it->second;
     }
 
+    // ---- selector trie + per-selector pattern lists (single-pass fast path) ----
+    struct TNode {
+        std::vector<std::pair<std::string, int32_t>> keys;  // (key, array_index)
+        std::vector<uint32_t> kids;
+        int16_t selector = -1;
+    };
+    std::vector<TNode> trie(1);
+    std::vector<std::vector<uint16_t>> sel_pats(sels.size());
+    uint64_t null_true[2] = {0, 0}, static_err[2] = {0, 0}, unsup[2] = {0, 0};
+    bool fast_ok = np <= kFastMaxPatterns && sels.size() <= kFastMaxSelectors;
+    for (size_t s = 0; s < sels.size() && fast_ok; s++) {
+        uint32_t cur = 0;
+        for (uint32_t k = 0; k < sels[s].comp_count; k++) {
+            const Component& c = comps[sels[s].comp_begin + k];
+            std::string key = lits.substr(c.lit_off, c.lit_len);
+            uint32_t next = 0;
+            bool found = false;
+            for (size_t j = 0; j < trie[cur].kids.size(); j++)
+                if (trie[cur].keys[j].first == key) { next = trie[cur].kids[j]; found = true; break; }
+            if (!found) {
+                for (size_t j = 0; j < trie[cur].keys.size(); j++)
+                    if (c.array_index >= 0 && trie[cur].keys[j].second == c.array_index) fast_ok = false;
+                next = (uint32_t)trie.size();
+                trie.push_back(TNode{});
+                trie[cur].keys.push_back({key, c.array_index});
+                trie[cur].kids.push_back(next);
+            }
+            cur = next;
+        }
+        trie[cur].selector = (int16_t)s;
+    }
+    if (trie.size() > kFastMaxNodes) fast_ok = false;
+    for (uint32_t i = 0; i < np; i++) {
+        const Pattern& p = pats[i];
+        const uint64_t bit = 1ull << (i & 63);
+        if (p.state == P_STATIC_E) { if (i < 128) static_err[i >> 6] |= bit; continue; }
+        if (p.state == P_UNSUPPORTED) { if (i < 128) unsup[i >> 6] |= bit; continue; }
+        if (p.selector < sels.size()) sel_pats[p.selector].push_back((uint16_t)i);
+        bool nt = false;  // Pattern.Matches on a Null result (String() == "", Array() == [])
+        switch (p.op) {
+            case OP_EQ: nt = p.lit_len == 0; break;
+            case OP_NEQ: nt = p.lit_len != 0; break;
+            case OP_INCL: nt = false; break;
+            case OP_EXCL: nt = true; break;
+            case OP_MATCHES: {
+                const RegexDfa& d = dfas[(size_t)dfa_of[i]];
+                nt = d.start == d.match_state || d.eot[d.start] != 0;
+                break;
+            }
+        }
+        if (nt && i < 128) null_true[i >> 6] |= bit;
+    }
+    if (fast_ok) flags |= kFlagFastOk;
+
     // ---- assemble ----
     Builder b;
     RulesetHdr hdr;
     std::memset(&hdr, 0, sizeof hdr);
     b.append(&hdr, sizeof hdr);
+    {
+        std::vector<TrieNode> tn(trie.size());
+        std::vector<TrieChild> tc;
+        for (size_t i = 0; i < trie.size(); i++) {
+            tn[i].child_begin = (uint16_t)tc.size();
+            tn[i].n_children = (uint8_t)trie[i].kids.size();
+            tn[i].flags = 0;
+            tn[i].selector = trie[i].selector;
+            tn[i].pad = 0;
+            for (size_t j = 0; j < trie[i].kids.size(); j++) {
+                TrieChild ch;
+                std::memset(&ch, 0, sizeof ch);
+                const std::string& key = trie[i].keys[j].first;
+                for (size_t q = 0; q < 4 && q < key.size(); q++) ch.prefix |= (uint32_t)(uint8_t)key[q] << (8 * q);
+                ch.key_len = (uint32_t)key.size();
+                ch.key_off = (uint32_t)lits.size();
+                lits += key;
+                ch.array_index = trie[i].keys[j].second;
+                if (ch.array_index >= 0) tn[i].flags |= 1;
+                ch.node = trie[i].kids[j];
+                tc.push_back(ch);
+            }
+        }
+        hdr.n_trie_nodes = (uint32_t)tn.size();
+        hdr.off_trie_nodes = (uint32_t)b.align16();
+        b.append(tn.data(), tn.size() * sizeof(TrieNode));
+        hdr.off_trie_children = (uint32_t)b.align16();
+        b.append(tc.data(), tc.size() * sizeof(TrieChild));
+        std::vector<SelectorPatterns> sp(sels.size());
+        std::vector<uint16_t> plist;
+        for (size_t s = 0; s < sels.size(); s++) {
+            sp[s].begin = (uint32_t)plist.size();
+            sp[s].count = (uint32_t)sel_pats[s].size();
+            sp[s].mask[0] = sp[s].mask[1] = 0;
+            for (uint16_t pi : sel_pats[s]) {
+                plist.push_back(pi);
+                if (pi < 128) sp[s].mask[pi >> 6] |= 1ull << (pi & 63);
+            }
+        }
+        hdr.off_sel_patterns = (uint32_t)b.align16();
+        b.append(sp.data(), sp.size() * sizeof(SelectorPatterns));
+        hdr.off_pattern_lists = (uint32_t)b.align16();
+        b.append(plist.data(), plist.size() * sizeof(uint16_t));
+        for (int k = 0; k < 2; k++) {
+            hdr.null_true[k] = null_true[k];
+            hdr.static_error[k] = static_err[k];
+            hdr.unsupported[k] = unsup[k];
+        }
+    }
     hdr.off_selectors = (uint32_t)b.align16();
     b.append(sels.data(), sels.size() * sizeof(Selector));
     hdr.off_components = (uint32_t)b.align16();

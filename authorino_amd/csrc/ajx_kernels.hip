@@ -1,30 +1,28 @@
 // ajx_kernels.hip — gfx950 kernels of the batched evaluator.
 //
-// ajx_eval_scan: one work-item per request (a wave evaluates 64 requests). For every
-// distinct selector of the request's ruleset it runs gj_get over the request's
-// document (the gjson scan), then evaluates every pattern on the resolved values
-// (Pattern.Matches), writes the per-pattern T bitmap and folds the And/Or tree into the
-// request's tri-state. Exact for arbitrary input bytes (well-formed or not).
+// ajx_eval_fast  one work-item per request: single pass over the document, all
+//                selectors followed at once through the ruleset trie, patterns
+//                evaluated as values complete, And/Or fold (ajx_fast.h). Requests it
+//                can not prove gjson-equivalent are appended to a slow list.
+// ajx_eval_scan  one work-item per request on the slow list (or on every request when
+//                forced): for each selector an exact gjson.Get scan (ajx_device.h gj_get),
+//                then the patterns and the fold. Exact for arbitrary input bytes.
 #include <hip/hip_runtime.h>
 
-#include "ajx_device.h"
+#include "ajx_fast.h"
 #include "ajx_kernels.h"
 
 namespace ajx {
 
-constexpr int kSelCache = 32;   // resolved selector values kept per request
-constexpr int kPatCache = 64;   // pattern results kept per request for the fold
+constexpr int kSelCache = 32;  // resolved selector values kept per request
+constexpr int kPatCache = 64;  // pattern results kept per request for the fold
 
-__global__ __launch_bounds__(256) void ajx_eval_scan(const uint8_t* const* __restrict__ sets,
-                                                     const uint32_t* __restrict__ set_of_req,
-                                                     const uint8_t* __restrict__ arena,
-                                                     const uint64_t* __restrict__ offs,
-                                                     const uint32_t* __restrict__ lens, uint32_t n,
-                                                     uint8_t* __restrict__ out_tri,
-                                                     int32_t* __restrict__ out_err,
-                                                     uint64_t* __restrict__ out_bm, uint32_t stride) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
+__device__ __forceinline__ void eval_scan_one(uint32_t r, const uint8_t* const* __restrict__ sets,
+                                              const uint32_t* __restrict__ set_of_req,
+                                              const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                                              const uint32_t* __restrict__ lens, uint8_t* __restrict__ out_tri,
+                                              int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
+                                              uint32_t stride) {
     const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const Selector* sels = reinterpret_cast<const Selector*>(blob + h->off_selectors);
@@ -43,8 +41,8 @@ __global__ __launch_bounds__(256) void ajx_eval_scan(const uint8_t* const* __res
             vals[s] = gj_get(doc, len, comps + sels[s].comp_begin, sels[s].comp_count, lits);
 
     auto value_of = [&](uint32_t p) -> ValueRef {
-        const Selector& s = sels[pats[p].selector];
         if (cache_sel) return vals[pats[p].selector];
+        const Selector& s = sels[pats[p].selector];
         return gj_get(doc, len, comps + s.comp_begin, s.comp_count, lits);
     };
     auto eval = [&](uint32_t p) -> uint8_t {
@@ -82,6 +80,72 @@ __global__ __launch_bounds__(256) void ajx_eval_scan(const uint8_t* const* __res
     if (out_err) out_err[r] = ep;
 }
 
+__global__ __launch_bounds__(256) void ajx_eval_scan(const uint8_t* const* __restrict__ sets,
+                                                     const uint32_t* __restrict__ set_of_req,
+                                                     const uint8_t* __restrict__ arena,
+                                                     const uint64_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ lens, uint32_t n,
+                                                     uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                                     uint64_t* __restrict__ out_bm, uint32_t stride) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    eval_scan_one(r, sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride);
+}
+
+// the slow list: grid-stride over the ids the fast kernel appended
+__global__ __launch_bounds__(256) void ajx_eval_scan_list(const uint8_t* const* __restrict__ sets,
+                                                          const uint32_t* __restrict__ set_of_req,
+                                                          const uint8_t* __restrict__ arena,
+                                                          const uint64_t* __restrict__ offs,
+                                                          const uint32_t* __restrict__ lens,
+                                                          const uint32_t* __restrict__ slow_count,
+                                                          const uint32_t* __restrict__ slow_ids,
+                                                          uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                                          uint64_t* __restrict__ out_bm, uint32_t stride) {
+    const uint32_t cnt = *slow_count;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x)
+        eval_scan_one(slow_ids[i], sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride);
+}
+
+__global__ __launch_bounds__(256) void ajx_eval_fast(const uint8_t* const* __restrict__ sets,
+                                                     const uint32_t* __restrict__ set_of_req,
+                                                     const uint8_t* __restrict__ arena,
+                                                     const uint64_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ lens, uint32_t n,
+                                                     uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                                     uint64_t* __restrict__ out_bm, uint32_t stride,
+                                                     uint32_t* __restrict__ slow_count,
+                                                     uint32_t* __restrict__ slow_ids) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    FastOut o;
+    if (h->flags & kFlagFastOk) fast_eval(blob, arena + offs[r], lens[r], &o);
+    else o.slow = true;
+    if (o.slow) {
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
+        return;
+    }
+    if (out_bm) {
+        uint64_t* row = out_bm + (size_t)r * stride;
+        for (uint32_t w = 0; w < stride; w++) row[w] = w < 2 ? o.t[w] : 0ull;
+    }
+    const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
+    int32_t ep;
+    const uint8_t t = run_fold(code, h->n_code,
+                               [&](uint32_t p) -> uint8_t {
+                                   const uint64_t bit = 1ull << (p & 63);
+                                   const uint32_t k = p >> 6;
+                                   if (h->static_error[k] & bit) return V_E;
+                                   if (o.u[k] & bit) return V_U;
+                                   return (o.t[k] & bit) ? V_T : V_F;
+                               },
+                               &ep);
+    out_tri[r] = t;
+    if (out_err) out_err[r] = ep;
+}
+
 hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
                             const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
                             int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream) {
@@ -90,6 +154,25 @@ hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_
     const uint32_t grid = (n + block - 1) / block;
     hipLaunchKernelGGL(ajx_eval_scan, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
                        d_lens, n, d_tri, d_err, d_bm, stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
+                            const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
+                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint32_t* d_slow_count,
+                            uint32_t* d_slow_ids, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t block = 256;
+    const uint32_t grid = (n + block - 1) / block;
+    hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ajx_eval_fast, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
+                       d_lens, n, d_tri, d_err, d_bm, stride, d_slow_count, d_slow_ids);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint32_t sgrid = grid < 2048 ? grid : 2048;
+    hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
+                       d_offs, d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
     return hipGetLastError();
 }
 

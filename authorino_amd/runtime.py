@@ -45,7 +45,8 @@ _lib_lock = threading.Lock()
 EXPORTS = [
     "authjx_init", "authjx_shutdown", "authjx_device_count", "authjx_compile", "authjx_free",
     "authjx_ruleset_patterns", "authjx_ruleset_selectors", "authjx_pattern_error",
-    "authjx_eval_batch_device", "authjx_eval_batch", "authjx_last_kernel_ms",
+    "authjx_eval_batch_device", "authjx_eval_batch", "authjx_last_kernel_ms", "authjx_set_exact_scan",
+    "authjx_last_exact_count",
 ]
 
 
@@ -57,6 +58,13 @@ def load_library(path: str = LIB_PATH):
             return _lib
         if not os.path.exists(path):
             raise AuthjxError(f"libauthjx.so not built at {path}: run __graft_entry__.build()")
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7. Loading torch
+        # first makes libauthjx.so bind to that copy (same soname), so HBM buffers and
+        # streams handed over from torch belong to the runtime that launches our kernels.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(path)
         L.authjx_init.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         L.authjx_init.restype = C.c_int
@@ -85,6 +93,10 @@ def load_library(path: str = LIB_PATH):
         L.authjx_eval_batch.restype = C.c_int
         L.authjx_last_kernel_ms.argtypes = [C.c_void_p]
         L.authjx_last_kernel_ms.restype = C.c_float
+        L.authjx_set_exact_scan.argtypes = [C.c_void_p, C.c_int]
+        L.authjx_set_exact_scan.restype = C.c_int
+        L.authjx_last_exact_count.argtypes = [C.c_void_p]
+        L.authjx_last_exact_count.restype = C.c_int64
         _lib = L
         return L
 
@@ -130,6 +142,14 @@ class Context:
             self._h, sarr, len(sets), ptr(set_of_req), ptr(arena), ptr(offs), ptr(lens), n,
             ptr(out_tri), ptr(out_err), ptr(out_bm), words, C.c_void_p(stream) if stream else None)
         _check(rc, "authjx_eval_batch_device")
+
+    def set_exact_scan(self, force: bool) -> None:
+        """Route every request through the exact scan kernel (for cross-checks)."""
+        _check(load_library().authjx_set_exact_scan(self._h, 1 if force else 0), "authjx_set_exact_scan")
+
+    def last_exact_count(self) -> int:
+        """Requests of the last batch the single-pass kernel handed to the exact scan."""
+        return int(load_library().authjx_last_exact_count(self._h))
 
     def last_kernel_ms(self) -> float:
         return float(load_library().authjx_last_kernel_ms(self._h))

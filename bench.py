@@ -99,7 +99,9 @@ def main():
     tri = torch.empty(w.n, dtype=torch.uint8, device=dev)
     err = torch.empty(w.n, dtype=torch.int32, device=dev)
     bm = torch.empty((w.n, words), dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream: the kernel and the timing events share it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
     def step():

@@ -141,6 +141,13 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
                       uint8_t* out_tristate, int32_t* out_err_idx, uint64_t* out_bitmap,
                       uint32_t bitmap_stride_words);
 
+/* Route every request through the exact per-selector scan kernel instead of the
+ * single-pass kernel (results are identical; used to cross-check the two paths). */
+int authjx_set_exact_scan(authjx_ctx* ctx, int force);
+/* Number of requests of the last batch the single-pass kernel handed to the exact scan
+ * (documents it could not prove gjson-equivalent, e.g. not valid JSON). Synchronises. */
+int64_t authjx_last_exact_count(authjx_ctx* ctx);
+
 /* Kernel-only timing of the last authjx_eval_batch_device on the context stream,
  * measured with HIP events around the dominant kernel (ms). */
 float authjx_last_kernel_ms(authjx_ctx* ctx);

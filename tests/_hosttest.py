@@ -134,3 +134,23 @@ class HostRegex:
     def __del__(self):
         if getattr(self, "_h", None):
             lib().ht_regex_free(self._h)
+
+
+def _fast_decl():
+    L = lib()
+    if not hasattr(L, "_fast_declared"):
+        L.ht_eval_fast.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8),
+                                   C.POINTER(C.c_int32)]
+        L.ht_eval_fast.restype = C.c_int
+        L._fast_declared = True
+    return L
+
+
+def eval_fast(hr: "HostRuleset", doc, mis: int = 0):
+    """Single-pass path on the host: (tri | -1 slow | -2 not eligible, err, res)."""
+    L = _fast_decl()
+    d = _b(doc)
+    res = (C.c_uint8 * max(hr.n, 1))()
+    err = C.c_int32(-1)
+    t = L.ht_eval_fast(hr._h, d, len(d), mis, res, C.byref(err))
+    return t, err.value, list(res)[: hr.n]

@@ -7,7 +7,7 @@
 #include <string>
 
 #include "../../authorino_amd/csrc/ajx_compiler.h"
-#include "../../authorino_amd/csrc/ajx_device.h"
+#include "../../authorino_amd/csrc/ajx_fast.h"
 #include "../../authorino_amd/csrc/ajx_regex.h"
 
 using namespace ajx;
@@ -122,3 +122,28 @@ int ht_regex_match(void* dv, const uint8_t* s, uint32_t n) {
 }
 
 }  // extern "C"
+
+extern "C" {
+// single-pass path: returns -1 when the document is handed to the exact scan, else the
+// tri-state; res[p] receives each pattern's value. `mis` places the copy at that
+// misalignment (0..15) like an arbitrary arena offset.
+int ht_eval_fast(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err) {
+    const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
+    const RulesetHdr* hd = (const RulesetHdr*)blob;
+    if (!(hd->flags & kFlagFastOk)) return -2;
+    std::vector<uint8_t> buf(len + 64);
+    uintptr_t base = ((uintptr_t)buf.data() + 15) & ~(uintptr_t)15;
+    uint8_t* d = (uint8_t*)base + (mis & 15);
+    std::memcpy(d, doc, len);
+    FastOut o;
+    fast_eval(blob, d, len, &o);
+    if (o.slow) return -1;
+    const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
+    for (uint32_t p = 0; p < hd->n_patterns; p++) {
+        uint64_t bit = 1ull << (p & 63);
+        uint32_t k = p >> 6;
+        res[p] = (hd->static_error[k] & bit) ? V_E : (o.u[k] & bit) ? V_U : (o.t[k] & bit) ? V_T : V_F;
+    }
+    return run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
+}
+}

@@ -148,3 +148,57 @@ def test_malformed_and_edge_documents(ctx):
     assert np.array_equal(tri[dec], otri[dec])
     assert np.array_equal(bm[dec], obm[dec])
     assert dec.mean() > 0.99
+
+
+def test_fast_and_exact_scan_kernels_agree(ctx):
+    """The single-pass kernel and the exact per-selector scan kernel give identical
+    outputs on the same batch (c3, 64 patterns incl. 8 regexes)."""
+    from authorino_amd import workloads as W
+
+    w = W.make("c3", n=20000, seed=21)
+    rs = ctx.compile_expression(w.expr)
+    tri, err, bm = ctx.eval_host_arena([rs], w.arena, w.offs, w.lens)
+    assert ctx.last_exact_count() == 0  # every synthetic doc took the single-pass path
+    ctx.set_exact_scan(True)
+    try:
+        tri2, err2, bm2 = ctx.eval_host_arena([rs], w.arena, w.offs, w.lens)
+    finally:
+        ctx.set_exact_scan(False)
+    assert np.array_equal(tri, tri2)
+    assert np.array_equal(err, err2)
+    assert np.array_equal(bm, bm2)
+
+
+def test_random_documents_and_selectors(ctx):
+    """Random JSON (escapes, arrays, duplicate keys, numbers, malformed bytes) and random
+    selector sets: GPU == oracle, per pattern and per tree."""
+    import fuzz_util as FU
+
+    rng = np.random.default_rng(77)
+    checked = 0
+    for _ in range(40):
+        pats = FU.rand_patterns(rng, int(rng.integers(1, 10)))
+        nodes = [(0, -1, -1, i) for i in range(len(pats))]
+        root = -1
+        for i in reversed(range(len(pats))):
+            nodes.append((2 if rng.random() < 0.3 else 1, i, root, -1))
+            root = len(nodes) - 1
+        ors = O.Ruleset(pats, nodes, root)
+        docs = []
+        for _ in range(200):
+            d = FU.rand_doc(rng)
+            docs.append(FU.mutate(rng, d) if rng.random() < 0.3 else d)
+        if any(ors.pattern(p, docs[0]) == O.UNSUPPORTED for p in range(len(pats))):
+            continue
+        rs = ctx.compile(pats, nodes, root)
+        tri, err, bm = ctx.eval_host([rs], docs)
+        lens = np.array([len(d) for d in docs], dtype=np.uint32)
+        offs = np.zeros(len(docs), dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1])
+        arena = np.frombuffer(b"".join(docs) + b"\0", dtype=np.uint8)
+        otri, oerr, obm = O.eval_batch([ors], arena, offs, lens)
+        dec = tri != 3
+        assert np.array_equal(tri[dec], otri[dec])
+        assert np.array_equal(bm[dec], obm[dec])
+        checked += int(dec.sum())
+    assert checked > 5000
