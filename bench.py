@@ -147,6 +147,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu, parity = cpu_baseline(w, R, args.cpu_seconds, tri.cpu().numpy(), bm.cpu().numpy().view(np.uint64))
     undecided = int((tri == runtime.UNDECIDED).sum().item())
+    exact_path = ctx.last_exact_count()  # requests the single-pass kernel handed to the exact scan
 
     if rank == 0:
         line = {
@@ -185,6 +186,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "undecided": undecided,
+            "exact_path_requests": exact_path,
         }
         print(json.dumps(line), flush=True)
     if dist:
