@@ -35,6 +35,8 @@ struct authjx_ctx {
     // requests the fast kernel hands to the exact scan
     uint32_t* d_slow = nullptr;  // [0] = count, [1..] = ids
     uint32_t slow_cap = 0;
+    uint64_t* d_rows = nullptr;  // stage-A capture rows
+    size_t rows_cap = 0;         // in u64
     int force_scan = 0;
     float last_ms = 0.f;
 };
@@ -109,6 +111,7 @@ void authjx_shutdown(authjx_ctx* ctx) {
     if (ctx->h_sets_pinned) (void)hipHostFree(ctx->h_sets_pinned);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_slow) (void)hipFree(ctx->d_slow);
+    if (ctx->d_rows) (void)hipFree(ctx->d_rows);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -168,26 +171,37 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     if (!ctx || !sets || n_sets == 0 || (n && (!d_arena || !d_offs || !d_lens || !d_out_tristate)))
         return AUTHJX_EINVAL;
     if (n_sets > 1 && !d_set_of_req) return AUTHJX_EINVAL;
-    uint32_t need_words = 0;
+    uint32_t need_words = 0, max_sel = 0;
     for (uint32_t i = 0; i < n_sets; i++) {
         if (!sets[i]) return AUTHJX_EINVAL;
         uint32_t w = (sets[i]->c.n_patterns + 63) / 64;
         if (w > need_words) need_words = w;
+        if (sets[i]->c.n_selectors > max_sel) max_sel = sets[i]->c.n_selectors;
     }
+    const uint32_t row_stride = 1 + max_sel;
     if (d_out_bitmap && bitmap_stride_words < need_words) return AUTHJX_EINVAL;
     std::lock_guard<std::mutex> lock(ctx->mu);
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     HIP_OK(hipSetDevice(ctx->device));
     int rc = ensure_sets(ctx, sets, n_sets, s);
     if (rc != AUTHJX_OK) return rc;
-    if (!ctx->force_scan && n > ctx->slow_cap) {
-        // growing the list: no batch in flight on this context may still use it
+    if (!ctx->force_scan && (n > ctx->slow_cap || (size_t)n * row_stride > ctx->rows_cap)) {
+        // growing the work buffers: no batch in flight on this context may still use them
         HIP_OK(hipStreamSynchronize(s));
-        if (ctx->d_slow) (void)hipFree(ctx->d_slow);
-        ctx->d_slow = nullptr;
-        ctx->slow_cap = 0;
-        HIP_OK(hipMalloc(&ctx->d_slow, ((size_t)n + 1) * sizeof(uint32_t)));
-        ctx->slow_cap = n;
+        if (n > ctx->slow_cap) {
+            if (ctx->d_slow) (void)hipFree(ctx->d_slow);
+            ctx->d_slow = nullptr;
+            ctx->slow_cap = 0;
+            HIP_OK(hipMalloc(&ctx->d_slow, ((size_t)n + 1) * sizeof(uint32_t)));
+            ctx->slow_cap = n;
+        }
+        if ((size_t)n * row_stride > ctx->rows_cap) {
+            if (ctx->d_rows) (void)hipFree(ctx->d_rows);
+            ctx->d_rows = nullptr;
+            ctx->rows_cap = 0;
+            HIP_OK(hipMalloc(&ctx->d_rows, (size_t)n * row_stride * sizeof(uint64_t)));
+            ctx->rows_cap = (size_t)n * row_stride;
+        }
     }
     HIP_OK(hipEventRecord(ctx->ev0, s));
     if (ctx->force_scan)
@@ -195,8 +209,8 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
     else
         HIP_OK(ajx::launch_eval_fast(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
-                                     d_out_err_idx, d_out_bitmap, bitmap_stride_words, ctx->d_slow, ctx->d_slow + 1,
-                                     s));
+                                     d_out_err_idx, d_out_bitmap, bitmap_stride_words, ctx->d_rows, row_stride,
+                                     ctx->d_slow, ctx->d_slow + 1, s));
     HIP_OK(hipEventRecord(ctx->ev1, s));
     return AUTHJX_OK;
 }

@@ -1,9 +1,11 @@
 // ajx_kernels.hip — gfx950 kernels of the batched evaluator.
 //
-// ajx_eval_fast  one work-item per request: single pass over the document, all
-//                selectors followed at once through the ruleset trie, patterns
-//                evaluated as values complete, And/Or fold (ajx_fast.h). Requests it
-//                can not prove gjson-equivalent are appended to a slow list.
+// ajx_scan_fast  stage A, one work-item per request: single pass over the document,
+//                all selectors followed at once through the ruleset trie; writes each
+//                selector's value span to the request's capture row (ajx_fast.h).
+//                Requests it can not prove gjson-equivalent go to a slow list.
+// ajx_patterns   stage B, one work-item per request: patterns on the captured values,
+//                T bitmap, And/Or fold.
 // ajx_eval_scan  one work-item per request on the slow list (or on every request when
 //                forced): for each selector an exact gjson.Get scan (ajx_device.h gj_get),
 //                then the patterns and the fold. Exact for arbitrary input bytes.
@@ -107,42 +109,70 @@ __global__ __launch_bounds__(256) void ajx_eval_scan_list(const uint8_t* const* 
         eval_scan_one(slow_ids[i], sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride);
 }
 
-__global__ __launch_bounds__(256) void ajx_eval_fast(const uint8_t* const* __restrict__ sets,
+// Stage A: structural scan -> capture rows (requests it can not handle -> slow list)
+__global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
                                                      const uint32_t* __restrict__ set_of_req,
                                                      const uint8_t* __restrict__ arena,
                                                      const uint64_t* __restrict__ offs,
                                                      const uint32_t* __restrict__ lens, uint32_t n,
-                                                     uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-                                                     uint64_t* __restrict__ out_bm, uint32_t stride,
+                                                     uint64_t* __restrict__ rows, uint32_t row_stride,
                                                      uint32_t* __restrict__ slow_count,
                                                      uint32_t* __restrict__ slow_ids) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    FastOut o;
-    if (h->flags & kFlagFastOk) fast_eval(blob, arena + offs[r], lens[r], &o);
-    else o.slow = true;
-    if (o.slow) {
-        slow_ids[atomicAdd(slow_count, 1u)] = r;
-        return;
+    uint64_t* row = rows + (size_t)r * row_stride;
+    const uint8_t* d = arena + offs[r];
+    const uint32_t len = lens[r];
+    bool ok = false;
+    if ((h->flags & kFlagFastOk) && len < (1u << 24)) {
+        const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
+        ok = scan_doc(blob, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
+            if (b < nblk) {
+                const uint4 v = a4[b];
+                return Block16{v.x, v.y, v.z, v.w};
+            }
+            return Block16{0u, 0u, 0u, 0u};
+        });
+    } else {
+        row[0] = kRowSlow;
     }
+    if (!ok) slow_ids[atomicAdd(slow_count, 1u)] = r;
+}
+
+// Stage B: patterns on the captured values, T bitmap, And/Or fold
+__global__ __launch_bounds__(256) void ajx_patterns(const uint8_t* const* __restrict__ sets,
+                                                    const uint32_t* __restrict__ set_of_req,
+                                                    const uint8_t* __restrict__ arena,
+                                                    const uint64_t* __restrict__ offs, uint32_t n,
+                                                    const uint64_t* __restrict__ rows, uint32_t row_stride,
+                                                    uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                                    uint64_t* __restrict__ out_bm, uint32_t stride) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint64_t* row = rows + (size_t)r * row_stride;
+    if (row[0] & kRowSlow) return;
+    const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    uint64_t t[2], u[2];
+    patterns_from_row(blob, arena + offs[r], row, t, u);
     if (out_bm) {
-        uint64_t* row = out_bm + (size_t)r * stride;
-        for (uint32_t w = 0; w < stride; w++) row[w] = w < 2 ? o.t[w] : 0ull;
+        uint64_t* orow = out_bm + (size_t)r * stride;
+        for (uint32_t w = 0; w < stride; w++) orow[w] = w < 2 ? t[w] : 0ull;
     }
     const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
     int32_t ep;
-    const uint8_t t = run_fold(code, h->n_code,
-                               [&](uint32_t p) -> uint8_t {
-                                   const uint64_t bit = 1ull << (p & 63);
-                                   const uint32_t k = p >> 6;
-                                   if (h->static_error[k] & bit) return V_E;
-                                   if (o.u[k] & bit) return V_U;
-                                   return (o.t[k] & bit) ? V_T : V_F;
-                               },
-                               &ep);
-    out_tri[r] = t;
+    const uint8_t tri = run_fold(code, h->n_code,
+                                 [&](uint32_t p) -> uint8_t {
+                                     const uint64_t bit = 1ull << (p & 63);
+                                     const uint32_t k = p >> 6;
+                                     if (h->static_error[k] & bit) return V_E;
+                                     if (u[k] & bit) return V_U;
+                                     return (t[k] & bit) ? V_T : V_F;
+                                 },
+                                 &ep);
+    out_tri[r] = tri;
     if (out_err) out_err[r] = ep;
 }
 
@@ -159,17 +189,19 @@ hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_
 
 hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
                             const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
-                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint32_t* d_slow_count,
-                            uint32_t* d_slow_ids, hipStream_t stream) {
+                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows, uint32_t row_stride,
+                            uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(ajx_eval_fast, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                       d_lens, n, d_tri, d_err, d_bm, stride, d_slow_count, d_slow_ids);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ajx_scan_fast, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
+                       d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(ajx_patterns, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs, n,
+                       d_rows, row_stride, d_tri, d_err, d_bm, stride);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t sgrid = grid < 2048 ? grid : 2048;
     hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
                        d_offs, d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);

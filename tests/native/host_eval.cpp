@@ -131,18 +131,24 @@ int ht_eval_fast(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
     const RulesetHdr* hd = (const RulesetHdr*)blob;
     if (!(hd->flags & kFlagFastOk)) return -2;
-    std::vector<uint8_t> buf(len + 64);
+    std::vector<uint8_t> buf(len + 64, 0);
     uintptr_t base = ((uintptr_t)buf.data() + 15) & ~(uintptr_t)15;
     uint8_t* d = (uint8_t*)base + (mis & 15);
     std::memcpy(d, doc, len);
-    FastOut o;
-    fast_eval(blob, d, len, &o);
-    if (o.slow) return -1;
+    std::vector<uint64_t> row(1 + hd->n_selectors, 0xDEADBEEFDEADBEEFull);
+    const uint32_t* a = (const uint32_t*)(d - mis);
+    bool ok = scan_doc(blob, d, len, row.data(), [&](uint32_t b, uint32_t nblk) -> Block16 {
+        if (b < nblk) return Block16{a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
+        return Block16{0, 0, 0, 0};
+    });
+    if (!ok) return -1;
+    uint64_t t[2], u[2];
+    patterns_from_row(blob, d, row.data(), t, u);
     const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
     for (uint32_t p = 0; p < hd->n_patterns; p++) {
         uint64_t bit = 1ull << (p & 63);
         uint32_t k = p >> 6;
-        res[p] = (hd->static_error[k] & bit) ? V_E : (o.u[k] & bit) ? V_U : (o.t[k] & bit) ? V_T : V_F;
+        res[p] = (hd->static_error[k] & bit) ? V_E : (u[k] & bit) ? V_U : (t[k] & bit) ? V_T : V_F;
     }
     return run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
 }
