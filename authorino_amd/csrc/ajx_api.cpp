@@ -38,6 +38,7 @@ struct authjx_ctx {
     uint64_t* d_rows = nullptr;  // stage-A capture rows
     size_t rows_cap = 0;         // in u64
     int force_scan = 0;
+    int ablate = 0;  // profiling only: run a reduced stage A (1 loads, 2 loads+classify)
     float last_ms = 0.f;
 };
 
@@ -210,8 +211,17 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     else
         HIP_OK(ajx::launch_eval_fast(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, ctx->d_rows, row_stride,
-                                     ctx->d_slow, ctx->d_slow + 1, s));
+                                     ctx->d_slow, ctx->d_slow + 1, s, ctx->ablate));
     HIP_OK(hipEventRecord(ctx->ev1, s));
+    return AUTHJX_OK;
+}
+
+// Profiling only (not in authjx.h): replace stage A by a reduced variant whose outputs
+// are meaningless, to price its parts (loads, classification) on the hardware.
+int authjx_debug_ablate(authjx_ctx* ctx, int mode) {
+    if (!ctx) return AUTHJX_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->ablate = mode;
     return AUTHJX_OK;
 }
 

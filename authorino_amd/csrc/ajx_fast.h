@@ -268,6 +268,7 @@ struct Scan {
     }
 
     // process the 16 document bytes of aligned block b (doc position of byte 0 = bpos)
+    template <int MODE = 0>
     AJX_HD void block(const Block16& blk, int32_t bpos) {
         const uint32_t x0 = blk.x, x1 = blk.y, x2 = blk.z, x3 = blk.w;
         uint32_t valid = 0xFFFFu;
@@ -315,6 +316,10 @@ struct Scan {
         if (mbs & outside) { st = X_SLOW; return; }  // backslash outside any string
         const uint32_t ns = outside & ~mst & ~mws;    // scalar bytes
         uint32_t toks = ((mst & outside) | qu) & 0xFFFFu;
+        if constexpr (MODE == 2) {  // ablation: classification only
+            gap_cnt += popc32(toks) + popc32(ns);
+            return;
+        }
         uint32_t below = 0;  // bits already consumed
         while (toks) {
             const uint32_t i = ctz32(toks);
@@ -345,7 +350,8 @@ struct Scan {
 
 // Stage A for one request. `row` = capture row (1 + n_selectors u64). Returns true
 // when the row is valid (false: the request needs the exact scan).
-template <class LoadBlock>
+// MODE (profiling ablations only): 0 = full scan, 1 = loads only, 2 = loads + classification
+template <int MODE = 0, class LoadBlock>
 AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t* row, LoadBlock load) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
     Scan s;
@@ -380,7 +386,11 @@ AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t b = b0 + (uint32_t)j;
-            if (b < nblk && s.st < X_DONE) s.block(cur[j], (int32_t)(b * 16) - (int32_t)mis);
+            if constexpr (MODE == 1) {
+                if (b < nblk) s.found ^= (uint64_t)(cur[j].x ^ cur[j].y ^ cur[j].z ^ cur[j].w) << j;
+            } else {
+                if (b < nblk && s.st < X_DONE) s.block<MODE>(cur[j], (int32_t)(b * 16) - (int32_t)mis);
+            }
         }
         if (s.st >= X_DONE) break;
 #pragma unroll
@@ -388,6 +398,10 @@ AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t
             cur[j] = nxt[j];
             nxt[j] = load(b0 + 8 + (uint32_t)j, nblk);
         }
+    }
+    if constexpr (MODE != 0) {
+        row[0] = s.found + s.gap_cnt;
+        return true;
     }
     if (s.st != X_DONE) {
         row[0] = kRowSlow;

@@ -18,6 +18,6 @@ namespace ajx {
 hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
                             const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
                             int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows, uint32_t row_stride,
-                            uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream);
+                            uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream, int ablate = 0);
 
 }  // namespace ajx

@@ -110,6 +110,7 @@ __global__ __launch_bounds__(256) void ajx_eval_scan_list(const uint8_t* const* 
 }
 
 // Stage A: structural scan -> capture rows (requests it can not handle -> slow list)
+template <int MODE>
 __global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
                                                      const uint32_t* __restrict__ set_of_req,
                                                      const uint8_t* __restrict__ arena,
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __res
     bool ok = false;
     if ((h->flags & kFlagFastOk) && len < (1u << 24)) {
         const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-        ok = scan_doc(blob, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
+        ok = scan_doc<MODE>(blob, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
             if (b < nblk) {
                 const uint4 v = a4[b];
                 return Block16{v.x, v.y, v.z, v.w};
@@ -190,14 +191,22 @@ hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_
 hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
                             const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
                             int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows, uint32_t row_stride,
-                            uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream) {
+                            uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream, int ablate) {
     if (n == 0) return hipSuccess;
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(ajx_scan_fast, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                       d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+    if (ablate == 1)
+        hipLaunchKernelGGL(ajx_scan_fast<1>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
+                           d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+    else if (ablate == 2)
+        hipLaunchKernelGGL(ajx_scan_fast<2>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
+                           d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+    else
+        hipLaunchKernelGGL(ajx_scan_fast<0>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
+                           d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+    if (ablate) return hipGetLastError();  // profiling ablation: stage A only
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(ajx_patterns, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs, n,
                        d_rows, row_stride, d_tri, d_err, d_bm, stride);
