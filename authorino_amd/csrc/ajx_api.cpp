@@ -172,6 +172,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     if (!ctx || !sets || n_sets == 0 || (n && (!d_arena || !d_offs || !d_lens || !d_out_tristate)))
         return AUTHJX_EINVAL;
     if (n_sets > 1 && !d_set_of_req) return AUTHJX_EINVAL;
+    if (n_sets == 1) d_set_of_req = nullptr;  // every request uses sets[0] (uniform-ruleset kernels)
     uint32_t need_words = 0, max_sel = 0;
     for (uint32_t i = 0; i < n_sets; i++) {
         if (!sets[i]) return AUTHJX_EINVAL;

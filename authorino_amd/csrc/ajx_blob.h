@@ -16,6 +16,12 @@
 #pragma once
 #include <stdint.h>
 
+#if defined(__HIPCC__)
+#define AJX_BLOB_HD __host__ __device__
+#else
+#define AJX_BLOB_HD
+#endif
+
 namespace ajx {
 
 constexpr uint32_t kMagic = 0x414A5842u;  // "AJXB"
@@ -90,14 +96,26 @@ struct TrieNode {
     uint16_t pad;
 };
 
+// A key is matched by (length, signature) where the signature is its last min(8, len)
+// bytes little-endian (key byte len-m+j in bits 8j..8j+7) — the bytes just before the
+// closing quote, which the scanner still holds in registers; longer keys then compare
+// their first len-8 bytes against the literal pool.
 struct TrieChild {
-    uint32_t prefix;       // first 4 key bytes, little-endian, zero padded
+    uint64_t sig;
     uint32_t key_len;
     uint32_t key_off;      // key bytes in the literal pool
     int32_t array_index;   // -1 never matches an element
     uint32_t node;
-    uint32_t pad[3];
 };
+static_assert(sizeof(TrieChild) == 24, "TrieChild layout");
+static_assert(sizeof(TrieNode) == 8, "TrieNode layout");
+
+AJX_BLOB_HD inline uint64_t key_signature(const uint8_t* key, uint32_t len) {
+    const uint32_t m = len < 8 ? len : 8;
+    uint64_t s = 0;
+    for (uint32_t j = 0; j < m; j++) s |= (uint64_t)key[len - m + j] << (8 * j);
+    return s;
+}
 
 struct SelectorPatterns {
     uint32_t begin;        // index into the uint16 pattern list

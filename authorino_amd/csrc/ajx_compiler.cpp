@@ -332,7 +332,7 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
                 TrieChild ch;
                 std::memset(&ch, 0, sizeof ch);
                 const std::string& key = trie[i].keys[j].first;
-                for (size_t q = 0; q < 4 && q < key.size(); q++) ch.prefix |= (uint32_t)(uint8_t)key[q] << (8 * q);
+                ch.sig = key_signature((const uint8_t*)key.data(), (uint32_t)key.size());
                 ch.key_len = (uint32_t)key.size();
                 ch.key_off = (uint32_t)lits.size();
                 lits += key;

@@ -56,15 +56,23 @@ struct Block16 {
     uint32_t x, y, z, w;
 };
 
-// Stage-A scanner state (kept in registers; no dynamically indexed arrays).
+// Stage-A scanner state (kept in registers; no dynamically indexed arrays). The trie
+// tables are read through `tn`/`tc`, which the kernel points at an LDS copy when the
+// whole batch uses one ruleset; document bytes a token needs (key tails, literals) come
+// from the previous/current block registers, global memory only on rare paths.
 struct Scan {
-    const uint8_t* blob;
     const TrieNode* tn;
     const TrieChild* tc;
     const uint8_t* lits;
     const uint8_t* d;
     uint64_t* row;  // capture row (header + records)
     uint32_t n;
+
+    uint64_t ph;        // bytes 8..15 of the previous 16-byte block
+    uint64_t cl, chh;   // bytes 0..7 / 8..15 of the current block
+    int32_t bpos;       // doc position of the current block's byte 0
+    uint32_t mbs;       // backslash bits of the current block
+    uint32_t carry_bs;  // last backslash before the current block (~0u none)
 
     uint64_t is_arr;    // bit k: container at depth k (1-based) is an array
     uint64_t nodes_lo;  // trie node per depth 1..8 (kNoNode = none)
@@ -79,11 +87,33 @@ struct Scan {
     // live arrays on selector paths (at most 2 nested): depth | h << 8
     uint32_t arr0, arr1, narr;
 
+    // (values are selected after they are computed, never by member address: that keeps
+    // the scanner state in registers)
+    AJX_HD static uint64_t funnel64(uint64_t a, uint64_t b, uint32_t sh) {  // ({b,a} >> sh) low 64, sh < 64
+        return sh ? (a >> sh) | (b << (64 - sh)) : a;
+    }
+    // the 8 document bytes ending just before current-block offset q (0..16), little-endian
+    AJX_HD uint64_t tail8(uint32_t q) const {
+        const uint64_t r1 = funnel64(ph, cl, (q & 7u) * 8);
+        const uint64_t r2 = funnel64(cl, chh, (q & 7u) * 8);
+        const uint64_t r3 = chh;
+        return q < 8 ? r1 : (q < 16 ? r2 : r3);
+    }
+    AJX_HD uint32_t byte_at(uint32_t i) const {
+        const uint64_t v0 = cl >> ((i & 7u) * 8), v1 = chh >> ((i & 7u) * 8);
+        return (uint32_t)(i < 8 ? v0 : v1) & 0xFFu;
+    }
+    AJX_HD uint32_t last_bs_before(uint32_t i) const {
+        const uint32_t mb = mbs & ((1u << i) - 1u);
+        return mb ? (uint32_t)(bpos + (int32_t)hibit32(mb)) : carry_bs;
+    }
+
     AJX_HD uint32_t node_at(uint32_t dd) const {
         if (dd == 0) return 0;
         if (dd > kFastDepth) return kNoNode;
         const uint32_t k = dd - 1;
-        const uint64_t w = k < 8 ? nodes_lo : nodes_hi;
+        const uint64_t lo = nodes_lo, hi = nodes_hi;
+        const uint64_t w = k < 8 ? lo : hi;
         return (uint32_t)((w >> ((k & 7) * 8)) & 0xFFu);
     }
     AJX_HD void set_node(uint32_t dd, uint32_t v) {
@@ -91,8 +121,12 @@ struct Scan {
         const uint32_t k = dd - 1;
         const uint64_t m = 0xFFull << ((k & 7) * 8);
         const uint64_t x = ((uint64_t)(v & 0xFF)) << ((k & 7) * 8);
-        if (k < 8) nodes_lo = (nodes_lo & ~m) | x;
-        else nodes_hi = (nodes_hi & ~m) | x;
+        // (both members stored unconditionally: stores into sibling members from two
+        // branches get merged into a store through a selected address, which would push
+        // the scanner state out of registers)
+        const uint64_t lo = nodes_lo, hi = nodes_hi;
+        nodes_lo = k < 8 ? (lo & ~m) | x : lo;
+        nodes_hi = k < 8 ? hi : (hi & ~m) | x;
     }
     AJX_HD bool top_is_arr() const { return (is_arr >> depth) & 1; }
     // trie node of the value about to start (key for objects, element index for arrays)
@@ -105,9 +139,9 @@ struct Scan {
         if (narr >= 2 && (arr1 & 0xFF) == depth) h = arr1 >> 8;
         else if (narr >= 1 && (arr0 & 0xFF) == depth) h = arr0 >> 8;
         else return kNoNode;
-        const TrieNode pn = tn[parent];
-        for (uint32_t c = 0; c < pn.n_children; c++)
-            if (tc[pn.child_begin + c].array_index == (int32_t)h) return tc[pn.child_begin + c].node;
+        const uint32_t cb = tn[parent].child_begin, nc = tn[parent].n_children;
+        for (uint32_t c = 0; c < nc; c++)
+            if (tc[cb + c].array_index == (int32_t)h) return tc[cb + c].node;
         return kNoNode;
     }
     AJX_HD int32_t leaf_sel(uint32_t node) const {
@@ -123,8 +157,11 @@ struct Scan {
     // a value (scalar, string or container) inside an array completed: next element
     AJX_HD void element_done() {
         if (!depth || !top_is_arr()) return;
-        if (narr >= 2 && (arr1 & 0xFF) == depth) arr1 += 0x100;
-        else if (narr >= 1 && (arr0 & 0xFF) == depth) arr0 += 0x100;
+        const uint32_t a0 = arr0, a1 = arr1;
+        const bool h1 = narr >= 2 && (a1 & 0xFF) == depth;
+        const bool h0 = !h1 && narr >= 1 && (a0 & 0xFF) == depth;
+        arr1 = a1 + (h1 ? 0x100u : 0u);
+        arr0 = a0 + (h0 ? 0x100u : 0u);
     }
     AJX_HD bool open_container(uint32_t c, uint32_t p) {
         const uint32_t node = value_node();
@@ -138,29 +175,37 @@ struct Scan {
         set_node(depth, live);
         if (s >= 0) {
             found |= 1ull << s;  // first match in document order wins
-            if (ncap == 0) { cap0 = (uint32_t)s | (depth << 8); cap0_start = p; }
-            else if (ncap == 1) { cap1 = (uint32_t)s | (depth << 8); cap1_start = p; }
-            else return false;
+            if (ncap >= 2) return false;
+            const uint32_t v = (uint32_t)s | (depth << 8), c0 = cap0, c1 = cap1, s0 = cap0_start, s1 = cap1_start;
+            cap0 = ncap == 0 ? v : c0;
+            cap0_start = ncap == 0 ? p : s0;
+            cap1 = ncap == 1 ? v : c1;
+            cap1_start = ncap == 1 ? p : s1;
             ncap++;
         }
         if (c == '[' && live != kNoNode && (tn[live].flags & 1)) {
-            if (narr == 0) arr0 = depth;
-            else if (narr == 1) arr1 = depth;
-            else return false;
+            if (narr >= 2) return false;
+            const uint32_t a0 = arr0, a1 = arr1;
+            arr0 = narr == 0 ? depth : a0;
+            arr1 = narr == 1 ? depth : a1;
             narr++;
         }
         st = c == '[' ? X_VALUE_OR_CLOSE : X_KEY_OR_CLOSE;
         return true;
     }
     AJX_HD void close_container(uint32_t p) {
-        if (ncap && (((ncap == 2 ? cap1 : cap0) >> 8) == depth)) {
-            const uint32_t cs = ncap == 2 ? cap1 : cap0;
-            const uint32_t start = ncap == 2 ? cap1_start : cap0_start;
+        // (copies first: a conditional over two lvalue members would select their
+        // addresses and force the state out of registers)
+        const uint32_t c0 = cap0, c1 = cap1, s0 = cap0_start, s1 = cap1_start, a0 = arr0, a1 = arr1;
+        const uint32_t cs = ncap == 2 ? c1 : c0;
+        if (ncap && (cs >> 8) == depth) {
+            const uint32_t start = ncap == 2 ? s1 : s0;
             row[1 + (cs & 0xFF)] =
                 (uint64_t)start | ((uint64_t)(((p + 1 - start) & 0xFFFFFFu) | ((uint32_t)T_JSON << 24)) << 32);
             ncap--;
         }
-        if (narr && (((narr == 2 ? arr1 : arr0) & 0xFF) == depth)) narr--;
+        const uint32_t at = narr == 2 ? a1 : a0;
+        if (narr && (at & 0xFF) == depth) narr--;
         depth--;
         st = depth == 0 ? X_DONE : X_COMMA_OR_CLOSE;
         element_done();  // the container was an element of its parent array
@@ -168,19 +213,31 @@ struct Scan {
     // a scalar occupying [gap_first, gap_last] completed in a value position
     AJX_HD bool scalar_value() {
         if (gap_last + 1 - gap_first != gap_cnt) return false;  // whitespace inside the run
-        const uint32_t c0 = d[gap_first];
+        const int32_t qend = (int32_t)gap_last + 1 - bpos;
+        const uint32_t m = gap_cnt < 8 ? gap_cnt : 8u;
+        uint64_t t8 = 0;  // the scalar's last m bytes in the top m bytes
+        if (qend >= 0) {
+            t8 = tail8((uint32_t)qend);
+        } else {  // trailing whitespace ran past a block boundary
+            for (uint32_t j = 0; j < m; j++) t8 |= (uint64_t)d[gap_last + 1 - m + j] << (8 * (8 - m + j));
+        }
+        uint32_t c0, c1;
+        if (gap_cnt <= 8) {
+            c0 = (uint32_t)(t8 >> (8 * (8 - gap_cnt))) & 0xFFu;
+            c1 = gap_cnt >= 2 ? (uint32_t)(t8 >> (8 * (9 - gap_cnt))) & 0xFFu : 0u;
+        } else {
+            c0 = d[gap_first];
+            c1 = d[gap_first + 1];
+        }
         uint32_t type;
-        const bool lit_n = c0 == 'n' && gap_cnt >= 2 && d[gap_first + 1] == 'u';
         if (c0 == 't') {
-            if (gap_cnt != 4 || d[gap_first + 1] != 'r' || d[gap_first + 2] != 'u' || d[gap_first + 3] != 'e') return false;
+            if (gap_cnt != 4 || (uint32_t)(t8 >> 32) != 0x65757274u) return false;  // "true"
             type = T_TRUE;
         } else if (c0 == 'f') {
-            if (gap_cnt != 5 || d[gap_first + 1] != 'a' || d[gap_first + 2] != 'l' || d[gap_first + 3] != 's' ||
-                d[gap_first + 4] != 'e')
-                return false;
+            if (gap_cnt != 5 || (t8 >> 24) != 0x65736C6166ull) return false;  // "false"
             type = T_FALSE;
-        } else if (lit_n) {
-            if (gap_cnt != 4 || d[gap_first + 2] != 'l' || d[gap_first + 3] != 'l') return false;
+        } else if (c0 == 'n' && c1 == 'u') {
+            if (gap_cnt != 4 || (uint32_t)(t8 >> 32) != 0x6C6C756Eu) return false;  // "null"
             type = T_NULL;
         } else if (c0 == '-' || c0 == '+' || (c0 >= '0' && c0 <= '9') || c0 == 'i' || c0 == 'I' || c0 == 'N' ||
                    c0 == 'n') {
@@ -194,28 +251,33 @@ struct Scan {
         st = X_COMMA_OR_CLOSE;
         return true;
     }
-    AJX_HD void key_closed(uint32_t p, uint32_t lb) {
-        const uint32_t ks = str_open + 1, klen = p - ks;
+    // closing quote of a key at block offset i (doc position p)
+    AJX_HD void key_closed(uint32_t p, uint32_t i) {
         pending = kNoNode;
         const uint32_t parent = node_at(depth);
         if (parent == kNoNode) return;
-        const TrieNode pn = tn[parent];
-        if (!pn.n_children) return;
+        const uint32_t nc = tn[parent].n_children;
+        if (!nc) return;
+        const uint32_t lb = last_bs_before(i);
         if (lb != ~0u && lb > str_open) { st = X_SLOW; return; }  // escaped key on a live path
-        uint32_t prefix = 0;
-        for (uint32_t k = 0; k < 4 && k < klen; k++) prefix |= (uint32_t)d[ks + k] << (8 * k);
-        for (uint32_t c = 0; c < pn.n_children; c++) {
-            const TrieChild ch = tc[pn.child_begin + c];
-            if (ch.key_len != klen || ch.prefix != prefix) continue;
+        const uint32_t ks = str_open + 1, klen = p - ks;
+        uint64_t sig = tail8(i);
+        if (klen < 8) sig = klen ? sig >> (8 * (8 - klen)) : 0ull;
+        const uint32_t cb = tn[parent].child_begin;
+        for (uint32_t c = 0; c < nc; c++) {
+            const TrieChild* ch = tc + cb + c;
+            if (ch->sig != sig || ch->key_len != klen) continue;
             bool eq = true;
-            for (uint32_t k = 4; k < klen; k++)
-                if (d[ks + k] != lits[ch.key_off + k]) { eq = false; break; }
-            if (eq) { pending = ch.node; return; }
+            const uint8_t* kl = lits + ch->key_off;
+            for (uint32_t k = 0; k + 8 < klen; k++)
+                if (d[ks + k] != kl[k]) { eq = false; break; }
+            if (eq) { pending = ch->node; return; }
         }
     }
 
-    // one token at doc position p (byte c); lb = last backslash before p
-    AJX_HD void token(uint32_t c, uint32_t p, uint32_t lb) {
+    // one token at block offset i (byte c)
+    AJX_HD void token(uint32_t c, uint32_t i) {
+        const uint32_t p = (uint32_t)(bpos + (int32_t)i);
         if (gap_cnt) {
             if ((st != X_VALUE && st != X_VALUE_OR_CLOSE) || !scalar_value() || (c != ',' && c != ']' && c != '}')) {
                 st = X_SLOW;
@@ -235,7 +297,7 @@ struct Scan {
                 return;
             case X_IN_KEY:  // c is the closing quote
                 st = X_COLON;
-                key_closed(p, lb);
+                key_closed(p, i);
                 return;
             case X_COLON:
                 st = c == ':' ? X_VALUE : X_SLOW;
@@ -252,7 +314,10 @@ struct Scan {
                 return;
             case X_IN_VAL: {
                 const int32_t s = leaf_sel(value_node());
-                if (s >= 0) record(s, str_open, p + 1, T_STRING, (lb != ~0u && lb > str_open) ? 1u : 0u);
+                if (s >= 0) {
+                    const uint32_t lb = last_bs_before(i);
+                    record(s, str_open, p + 1, T_STRING, (lb != ~0u && lb > str_open) ? 1u : 0u);
+                }
                 element_done();
                 st = X_COMMA_OR_CLOSE;
                 return;
@@ -267,17 +332,21 @@ struct Scan {
         }
     }
 
-    // process the 16 document bytes of aligned block b (doc position of byte 0 = bpos)
+    // process the 16 document bytes of aligned block `blk` (doc position of byte 0 = bp)
     template <int MODE = 0>
-    AJX_HD void block(const Block16& blk, int32_t bpos) {
-        const uint32_t x0 = blk.x, x1 = blk.y, x2 = blk.z, x3 = blk.w;
+    AJX_HD void block(const Block16& blk, int32_t bp) {
+        ph = chh;
+        cl = (uint64_t)blk.x | ((uint64_t)blk.y << 32);
+        chh = (uint64_t)blk.z | ((uint64_t)blk.w << 32);
+        bpos = bp;
         uint32_t valid = 0xFFFFu;
-        if (bpos < 0) valid &= 0xFFFFu << (uint32_t)(-bpos);
-        if (bpos + 16 > (int32_t)n) valid &= 0xFFFFu >> (uint32_t)(bpos + 16 - (int32_t)n);
-        uint32_t mq = 0, mbs = 0, mst = 0, mws = 0;
+        if (bp < 0) valid &= 0xFFFFu << (uint32_t)(-bp);
+        if (bp + 16 > (int32_t)n) valid &= 0xFFFFu >> (uint32_t)(bp + 16 - (int32_t)n);
+        uint32_t mq = 0, mst = 0, mws = 0;
+        mbs = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const uint32_t x = k == 0 ? x0 : k == 1 ? x1 : k == 2 ? x2 : x3;
+            const uint32_t x = k == 0 ? blk.x : k == 1 ? blk.y : k == 2 ? blk.z : blk.w;
             const uint32_t lx = x | 0x20202020u;
             mq |= gather4(eq_bytes(x, 0x22222222u)) << (4 * k);
             mbs |= gather4(eq_bytes(x, 0x5C5C5C5Cu)) << (4 * k);
@@ -301,8 +370,8 @@ struct Scan {
             esc = (seq >> 16) & 1u;
             escaped = (even ^ ((seq << 1) & 0xFFFFu)) & follows;
         }
-        const uint32_t carry_bs = last_bs;
-        if (mbs) last_bs = (uint32_t)(bpos + (int32_t)hibit32(mbs));
+        carry_bs = last_bs;
+        if (mbs) last_bs = (uint32_t)(bp + (int32_t)hibit32(mbs));
         const uint32_t qu = mq & ~escaped;
         uint32_t x = qu;
         x ^= x << 1;
@@ -326,22 +395,18 @@ struct Scan {
             toks &= toks - 1;
             const uint32_t g = ns & ((1u << i) - 1u) & ~below;
             if (g) {
-                if (gap_cnt == 0) gap_first = (uint32_t)(bpos + (int32_t)ctz32(g));
-                gap_last = (uint32_t)(bpos + (int32_t)hibit32(g));
+                if (gap_cnt == 0) gap_first = (uint32_t)(bp + (int32_t)ctz32(g));
+                gap_last = (uint32_t)(bp + (int32_t)hibit32(g));
                 gap_cnt += popc32(g);
             }
             below = (2u << i) - 1u;
-            const uint32_t wsel = i < 8 ? (i < 4 ? x0 : x1) : (i < 12 ? x2 : x3);
-            const uint32_t c = (wsel >> ((i & 3) * 8)) & 0xFFu;
-            const uint32_t mb = mbs & ((1u << i) - 1u);
-            const uint32_t lb = mb ? (uint32_t)(bpos + (int32_t)hibit32(mb)) : carry_bs;
-            token(c, (uint32_t)(bpos + (int32_t)i), lb);
+            token(byte_at(i), i);
             if (st >= X_DONE) return;
         }
         const uint32_t g = ns & ~below & 0xFFFFu;
         if (g) {
-            if (gap_cnt == 0) gap_first = (uint32_t)(bpos + (int32_t)ctz32(g));
-            gap_last = (uint32_t)(bpos + (int32_t)hibit32(g));
+            if (gap_cnt == 0) gap_first = (uint32_t)(bp + (int32_t)ctz32(g));
+            gap_last = (uint32_t)(bp + (int32_t)hibit32(g));
             gap_cnt += popc32(g);
             if (st == X_ROOT) st = X_SLOW;  // a scalar (or junk) before the root container
         }
@@ -349,19 +414,24 @@ struct Scan {
 };
 
 // Stage A for one request. `row` = capture row (1 + n_selectors u64). Returns true
-// when the row is valid (false: the request needs the exact scan).
+// when the row is valid (false: the request needs the exact scan). `tn`/`tc` are the
+// ruleset's trie tables (an LDS copy or the blob's own).
 // MODE (profiling ablations only): 0 = full scan, 1 = loads only, 2 = loads + classification
 template <int MODE = 0, class LoadBlock>
-AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t* row, LoadBlock load) {
+AJX_HD bool scan_doc(const uint8_t* blob, const TrieNode* tn, const TrieChild* tc, const uint8_t* d, uint32_t n,
+                     uint64_t* row, LoadBlock load) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
     Scan s;
-    s.blob = blob;
-    s.tn = (const TrieNode*)(blob + h->off_trie_nodes);
-    s.tc = (const TrieChild*)(blob + h->off_trie_children);
+    s.tn = tn;
+    s.tc = tc;
     s.lits = blob + h->off_literals;
     s.d = d;
     s.row = row;
     s.n = n;
+    s.ph = s.cl = s.chh = 0;
+    s.bpos = 0;
+    s.mbs = 0;
+    s.carry_bs = ~0u;
     s.is_arr = 0;
     s.nodes_lo = s.nodes_hi = ~0ull;
     s.found = 0;
@@ -383,14 +453,19 @@ AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t
 #pragma unroll
     for (int j = 0; j < 4; j++) nxt[j] = load((uint32_t)(4 + j), nblk);
     for (uint32_t b0 = 0; b0 < nblk; b0 += 4) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t b = b0 + (uint32_t)j;
+        // one copy of the block body (the window shifts down instead of unrolling j:
+        // the token machine is large and four inlined copies thrash the I-cache)
+#pragma unroll 1
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t b = b0 + j;
             if constexpr (MODE == 1) {
-                if (b < nblk) s.found ^= (uint64_t)(cur[j].x ^ cur[j].y ^ cur[j].z ^ cur[j].w) << j;
+                if (b < nblk) s.found ^= (uint64_t)(cur[0].x ^ cur[0].y ^ cur[0].z ^ cur[0].w) << j;
             } else {
-                if (b < nblk && s.st < X_DONE) s.block<MODE>(cur[j], (int32_t)(b * 16) - (int32_t)mis);
+                if (b < nblk && s.st < X_DONE) s.block<MODE>(cur[0], (int32_t)(b * 16) - (int32_t)mis);
             }
+            cur[0] = cur[1];
+            cur[1] = cur[2];
+            cur[2] = cur[3];
         }
         if (s.st >= X_DONE) break;
 #pragma unroll
@@ -409,6 +484,13 @@ AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t
     }
     row[0] = s.found;
     return true;
+}
+
+template <int MODE = 0, class LoadBlock>
+AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t* row, LoadBlock load) {
+    const RulesetHdr* h = (const RulesetHdr*)blob;
+    return scan_doc<MODE>(blob, (const TrieNode*)(blob + h->off_trie_nodes),
+                          (const TrieChild*)(blob + h->off_trie_children), d, n, row, load);
 }
 
 // Stage B for one request: patterns on the captured values, bitmap, fold.

@@ -109,8 +109,10 @@ __global__ __launch_bounds__(256) void ajx_eval_scan_list(const uint8_t* const* 
         eval_scan_one(slow_ids[i], sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride);
 }
 
-// Stage A: structural scan -> capture rows (requests it can not handle -> slow list)
-template <int MODE>
+// Stage A: structural scan -> capture rows (requests it can not handle -> slow list).
+// SHARED: the whole batch uses sets[0]; its trie tables are copied to LDS once per
+// workgroup so the token loop never touches global memory for them.
+template <int MODE, bool SHARED>
 __global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
                                                      const uint32_t* __restrict__ set_of_req,
                                                      const uint8_t* __restrict__ arena,
@@ -119,17 +121,34 @@ __global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __res
                                                      uint64_t* __restrict__ rows, uint32_t row_stride,
                                                      uint32_t* __restrict__ slow_count,
                                                      uint32_t* __restrict__ slow_ids) {
+    __shared__ uint32_t s_tab[SHARED ? (kFastMaxNodes * (sizeof(TrieNode) + sizeof(TrieChild))) / 4 : 1];
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
-    const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
+    const uint8_t* blob = sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)];
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    const TrieNode* tn = reinterpret_cast<const TrieNode*>(blob + h->off_trie_nodes);
+    const TrieChild* tc = reinterpret_cast<const TrieChild*>(blob + h->off_trie_children);
+    const bool fast_ok = (h->flags & kFlagFastOk) != 0;
+    if constexpr (SHARED) {
+        if (fast_ok) {  // uniform over the workgroup
+            const uint32_t nn = h->n_trie_nodes;
+            const uint32_t wn = nn * (sizeof(TrieNode) / 4), wc = (nn - 1) * (sizeof(TrieChild) / 4);
+            const uint32_t* gn = reinterpret_cast<const uint32_t*>(tn);
+            const uint32_t* gc = reinterpret_cast<const uint32_t*>(tc);
+            for (uint32_t i = threadIdx.x; i < wn; i += blockDim.x) s_tab[i] = gn[i];
+            for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) s_tab[kFastMaxNodes * 2 + i] = gc[i];
+        }
+        __syncthreads();
+        tn = reinterpret_cast<const TrieNode*>(s_tab);  // unconditionally LDS: ds_read in the scan
+        tc = reinterpret_cast<const TrieChild*>(s_tab + kFastMaxNodes * 2);
+    }
+    if (r >= n) return;
     uint64_t* row = rows + (size_t)r * row_stride;
     const uint8_t* d = arena + offs[r];
     const uint32_t len = lens[r];
     bool ok = false;
-    if ((h->flags & kFlagFastOk) && len < (1u << 24)) {
+    if (fast_ok && len < (1u << 24)) {
         const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-        ok = scan_doc<MODE>(blob, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
+        ok = scan_doc<MODE>(blob, tn, tc, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
             if (b < nblk) {
                 const uint4 v = a4[b];
                 return Block16{v.x, v.y, v.z, v.w};
@@ -140,6 +159,79 @@ __global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __res
         row[0] = kRowSlow;
     }
     if (!ok) slow_ids[atomicAdd(slow_count, 1u)] = r;
+}
+
+// Stages A+B fused: the patterns run right after the scan, while the request's value
+// bytes are still in L2 / MALL (stage B alone re-reads them from HBM).
+template <bool SHARED>
+__global__ __launch_bounds__(256) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
+                                                      const uint32_t* __restrict__ set_of_req,
+                                                      const uint8_t* __restrict__ arena,
+                                                      const uint64_t* __restrict__ offs,
+                                                      const uint32_t* __restrict__ lens, uint32_t n,
+                                                      uint64_t* __restrict__ rows, uint32_t row_stride,
+                                                      uint32_t* __restrict__ slow_count,
+                                                      uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
+                                                      int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
+                                                      uint32_t stride) {
+    __shared__ uint32_t s_tab[SHARED ? (kFastMaxNodes * (sizeof(TrieNode) + sizeof(TrieChild))) / 4 : 1];
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint8_t* blob = sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)];
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    const TrieNode* tn = reinterpret_cast<const TrieNode*>(blob + h->off_trie_nodes);
+    const TrieChild* tc = reinterpret_cast<const TrieChild*>(blob + h->off_trie_children);
+    const bool fast_ok = (h->flags & kFlagFastOk) != 0;
+    if constexpr (SHARED) {
+        if (fast_ok) {
+            const uint32_t nn = h->n_trie_nodes;
+            const uint32_t wn = nn * (sizeof(TrieNode) / 4), wc = (nn - 1) * (sizeof(TrieChild) / 4);
+            const uint32_t* gn = reinterpret_cast<const uint32_t*>(tn);
+            const uint32_t* gc = reinterpret_cast<const uint32_t*>(tc);
+            for (uint32_t i = threadIdx.x; i < wn; i += blockDim.x) s_tab[i] = gn[i];
+            for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) s_tab[kFastMaxNodes * 2 + i] = gc[i];
+        }
+        __syncthreads();
+        tn = reinterpret_cast<const TrieNode*>(s_tab);
+        tc = reinterpret_cast<const TrieChild*>(s_tab + kFastMaxNodes * 2);
+    }
+    if (r >= n) return;
+    uint64_t* row = rows + (size_t)r * row_stride;
+    const uint8_t* d = arena + offs[r];
+    const uint32_t len = lens[r];
+    bool ok = false;
+    if (fast_ok && len < (1u << 24)) {
+        const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
+        ok = scan_doc<0>(blob, tn, tc, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
+            if (b < nblk) {
+                const uint4 v = a4[b];
+                return Block16{v.x, v.y, v.z, v.w};
+            }
+            return Block16{0u, 0u, 0u, 0u};
+        });
+    }
+    if (!ok) {
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
+        return;
+    }
+    uint64_t t[2], u[2];
+    patterns_from_row(blob, d, row, t, u);
+    if (out_bm) {
+        uint64_t* orow = out_bm + (size_t)r * stride;
+        for (uint32_t w = 0; w < stride; w++) orow[w] = w < 2 ? t[w] : 0ull;
+    }
+    const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
+    int32_t ep;
+    const uint8_t tri = run_fold(code, h->n_code,
+                                 [&](uint32_t p) -> uint8_t {
+                                     const uint64_t bit = 1ull << (p & 63);
+                                     const uint32_t k = p >> 6;
+                                     if (h->static_error[k] & bit) return V_E;
+                                     if (u[k] & bit) return V_U;
+                                     return (t[k] & bit) ? V_T : V_F;
+                                 },
+                                 &ep);
+    out_tri[r] = tri;
+    if (out_err) out_err[r] = ep;
 }
 
 // Stage B: patterns on the captured values, T bitmap, And/Or fold
@@ -197,15 +289,27 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     const uint32_t grid = (n + block - 1) / block;
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    if (ablate == 1)
-        hipLaunchKernelGGL(ajx_scan_fast<1>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                           d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
-    else if (ablate == 2)
-        hipLaunchKernelGGL(ajx_scan_fast<2>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                           d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
-    else
-        hipLaunchKernelGGL(ajx_scan_fast<0>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                           d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+    const bool shared = d_set_of_req == nullptr;
+#define AJX_SCAN(M, S)                                                                                      \
+    hipLaunchKernelGGL((ajx_scan_fast<M, S>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, \
+                       d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids)
+    if (ablate == 3 || ablate == 4) {
+    } else if (ablate == 1) AJX_SCAN(1, true);
+    else if (ablate == 2) AJX_SCAN(2, true);
+    else if (shared) AJX_SCAN(0, true);
+    else AJX_SCAN(0, false);
+#undef AJX_SCAN
+    if (ablate == 3 || ablate == 4) {  // fused A+B (4: per-request ruleset table)
+        if (ablate == 3)
+            hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
+                               d_bm, stride);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        const uint32_t sgrid = grid < 2048 ? grid : 2048;
+        hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
+        return hipGetLastError();
+    }
     if (ablate) return hipGetLastError();  // profiling ablation: stage A only
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(ajx_patterns, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs, n,

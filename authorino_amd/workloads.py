@@ -81,13 +81,13 @@ def _make_doc(rng: np.random.Generator, target_len: int, uid: int) -> bytes:
     method = "GET" if p[0] < 0.95 else rng.choice(["POST", "PUT", "DELETE"])
     sub = "user-%04d" % (uid % 10000) if p[1] < 0.95 else "user-0000"
     headers = {}
-    for name in rng.choice(HEADER_NAMES, size=int(rng.integers(3, 9)), replace=False):
-        headers[str(name)] = _hex(rng, int(rng.integers(4, 16)))
+    for name in rng.choice(HEADER_NAMES, size=int(rng.integers(1, 5)), replace=False):
+        headers[str(name)] = _hex(rng, int(rng.integers(4, 13)))
     headers["x-tenant"] = "acme" if p[2] < 0.95 else "globex"
     if p[3] >= 0.95:
         headers["x-blocked"] = "1"
     headers["authorization"] = "Bearer " + _hex(rng, 16)
-    headers["user-agent"] = "Mozilla/5.0 (X11; Linux x86_64) curl/8.%d & friends <bot>" % int(rng.integers(0, 9))
+    headers["user-agent"] = "Mozilla/5.0 curl/8.%d <bot>" % int(rng.integers(0, 9))
     headers[":path"] = "/api/v%d/orders/%d" % (int(rng.integers(1, 4)), int(rng.integers(1, 100000)))
     host = "api.example.com" if p[4] < 0.95 else "api.example.org"
     path = headers[":path"] if p[5] < 0.95 else "/admin/metrics"
@@ -116,12 +116,25 @@ def _make_doc(rng: np.random.Generator, target_len: int, uid: int) -> bytes:
                                                               "portValue": int(rng.integers(1024, 65535))}}},
                     "request": {"time": {"seconds": int(1700000000 + uid)}, "http": http}},
         "request": {"host": host, "method": str(method), "path": path, "url_path": path.split("?")[0],
-                    "headers": go_map({"authorization": headers["authorization"]})},
+                    },
         "source": {"address": "10.0.0.%d" % int(rng.integers(1, 250)) if p[14] < 0.95 else "10.66.6.6"},
         "destination": {"address": "10.1.0.1", "port": 8080},
         "auth": {"identity": identity, "metadata": go_map({"tenant": {"plan": "gold" if p[15] < 0.95 else "free"}})},
     }
     s = go_json(doc)
+    # over the target: drop optional parts (random headers first, then Envoy metadata
+    # no selector reads) until it fits or nothing optional is left
+    optional = [k for k in headers if k not in ("x-tenant", "x-blocked", "authorization", "user-agent", ":path")]
+    while len(s) > target_len and optional:
+        del headers[optional.pop()]
+        http["headers"] = go_map(headers)
+        s = go_json(doc)
+    for drop in (lambda: doc["context"].pop("source"), lambda: doc["context"]["request"].pop("time"),
+                 lambda: http.pop("id")):
+        if len(s) <= target_len:
+            break
+        drop()
+        s = go_json(doc)
     # pad (a header value) to the target length
     short = target_len - len(s)
     if short > 20:

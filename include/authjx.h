@@ -120,7 +120,7 @@ size_t authjx_pattern_error(const authjx_ruleset* rs, uint32_t i, char* buf, siz
 
 /* Evaluate a batch whose documents are already in device memory (HBM).
  *   sets[n_sets]      rulesets; request r uses sets[set_of_req ? set_of_req[r] : 0]
- *   d_set_of_req      device u32[n] or NULL
+ *   d_set_of_req      device u32[n] (entries < n_sets) or NULL; ignored when n_sets == 1
  *   d_arena           device bytes; document r = d_arena[d_offs[r] .. + d_lens[r])
  *   d_out_tristate    device u8[n]  (AUTHJX_F/T/E/UNDECIDED)
  *   d_out_err_idx     device i32[n] pattern whose error decided an E, else -1 (may be NULL)

@@ -1,5 +1,5 @@
 """Profiling helper: time stage A of the single-pass path in its ablation variants
-(0 full scan, 1 loads only, 2 loads + classification) on the c2 workload, interleaved
+(0 full split path, 1 loads only, 2 loads + classification, 3 fused scan+patterns) on the c2 workload, interleaved
 in one process (cdna_hip_programming.md §5.4 rule 24). Prints one JSON line."""
 import ctypes as C
 import json
@@ -31,8 +31,9 @@ bm = torch.empty((n, (R + 63) // 64), dtype=torch.int64, device=dev)
 stream = torch.cuda.Stream(dev)
 torch.cuda.set_stream(stream)
 res = {0: [], 1: [], 2: [], 3: []}
+outs = {}
 for rep in range(6):
-    for mode in (0, 1, 2):
+    for mode in (0, 1, 2, 3):
         L.authjx_debug_ablate(ctx._h, mode)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
@@ -41,6 +42,9 @@ for rep in range(6):
         torch.cuda.synchronize()
         if rep:
             res[mode].append(a.elapsed_time(b))
+        if mode in (0, 3) and rep == 1:
+            outs[mode] = (tri.cpu().numpy().copy(), bm.cpu().numpy().copy())
 bytes_ = int(w.lens.astype(np.int64).sum())
 out = {m: {"ms": float(np.median(v)), "GBps": bytes_ / (np.median(v) * 1e-3) / 1e9} for m, v in res.items() if v}
-print(json.dumps({"workload": wl, "n": n, "doc_bytes": bytes_, "modes": out}))
+same = bool(np.array_equal(outs[0][0], outs[3][0]) and np.array_equal(outs[0][1], outs[3][1]))
+print(json.dumps({"workload": wl, "n": n, "doc_bytes": bytes_, "modes": out, "fused_equals_split": same}))

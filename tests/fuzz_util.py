@@ -98,3 +98,26 @@ def mutate(rng, d: bytes) -> bytes:
         i = int(rng.integers(0, len(d)))
         d[i:i] = bytes(rng.choice([b"\\", b'"', b"1", b"{", b"]", b"x"]))
     return bytes(d)
+
+
+def _ws(rng):
+    return "".join(str(rng.choice([" ", "\n", "\t", "\r"])) for _ in range(int(rng.integers(0, 3)) * int(rng.integers(0, 12))))
+
+
+def dump_ws(v, rng):
+    """Like dump() but with whitespace runs of 0..22 bytes around every token (scalars
+    and keys whose bytes straddle 16-byte blocks, literals followed by long runs)."""
+    t, x = v
+    if t == "s":
+        return json.dumps(x, ensure_ascii=bool(rng.integers(0, 2)))
+    if t in ("n", "l"):
+        return x
+    w = lambda: _ws(rng)  # noqa: E731
+    if t == "o":
+        return "{" + w() + ",".join(w() + json.dumps(k) + w() + ":" + w() + dump_ws(val, rng) + w() for k, val in x) + w() + "}"
+    return "[" + w() + ",".join(w() + dump_ws(val, rng) + w() for val in x) + w() + "]"
+
+
+def rand_doc_ws(rng):
+    v = ("o", [(KEYS[rng.integers(0, len(KEYS))], rand_value(rng, 4)) for _ in range(int(rng.integers(1, 7)))])
+    return (_ws(rng) + dump_ws(v, rng) + _ws(rng)).encode("utf-8")

@@ -45,3 +45,25 @@ def test_fuzz_scan_and_fast_match_oracle(seed):
                 assert fres == ot, (pats, d)
                 assert tf == t_or, (pats, d)
     assert n_fast > 300
+
+
+@pytest.mark.parametrize("seed", [10, 11])
+def test_fuzz_fast_whitespace_runs(seed):
+    """Single-pass path on valid documents with long whitespace runs between tokens."""
+    rng = np.random.default_rng(seed)
+    n_fast = 0
+    for _ in range(150):
+        pats = FU.rand_patterns(rng, int(rng.integers(1, 8)))
+        nodes, root = _chain(len(pats))
+        rs = O.Ruleset(pats, nodes, root)
+        hr = H.HostRuleset(pats, nodes, root)
+        for _ in range(8):
+            d = FU.rand_doc_ws(rng)
+            ot = [rs.pattern(p, d) for p in range(len(pats))]
+            if O.UNSUPPORTED in ot:
+                continue
+            tf, _, fres = H.eval_fast(hr, d, mis=int(rng.integers(0, 16)))
+            if tf >= 0 and 3 not in fres:
+                n_fast += 1
+                assert fres == ot, (pats, d)
+    assert n_fast > 300
