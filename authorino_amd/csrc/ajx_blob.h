@@ -117,6 +117,25 @@ AJX_BLOB_HD inline uint64_t key_signature(const uint8_t* key, uint32_t len) {
     return s;
 }
 
+// Key lookup for the single-pass path: every (parent node, key) edge of the trie in
+// one open-addressing table (linear probing), so a closing key quote costs one 16-byte
+// LDS read instead of a walk over the parent's children.
+struct KeySlot {
+    uint64_t sig;      // key_signature(key)
+    uint32_t meta;     // key_len | parent << 16 | node << 24; kEmptySlot = free
+    uint32_t key_off;  // key bytes in the literal pool
+};
+static_assert(sizeof(KeySlot) == 16, "KeySlot layout");
+constexpr uint32_t kEmptySlot = 0xFFFFFFFFu;
+constexpr uint32_t kMaxKeySlotsLog2 = 9;
+
+AJX_BLOB_HD inline uint32_t key_slot_hash(uint64_t sig, uint32_t klen, uint32_t parent, uint32_t log2) {
+    uint32_t x = (uint32_t)sig ^ (((uint32_t)(sig >> 32) << 13) | ((uint32_t)(sig >> 32) >> 19)) ^ (klen << 24) ^
+                 (parent << 16);
+    x *= 0x9E3779B1u;
+    return x >> (32 - log2);
+}
+
 struct SelectorPatterns {
     uint32_t begin;        // index into the uint16 pattern list
     uint32_t count;
@@ -143,7 +162,9 @@ struct RulesetHdr {
     uint32_t off_trie_children;
     uint32_t off_sel_patterns;  // SelectorPatterns[n_selectors]
     uint32_t off_pattern_lists; // uint16_t[]
-    uint32_t pad0;
+    uint32_t key_slots_log2;    // KeySlot table of 1 << key_slots_log2 entries
+    uint32_t off_key_slots;
+    uint32_t pad1[3];
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
     uint64_t unsupported[2];    // pattern p can not be decided on the device

@@ -342,11 +342,29 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
                 tc.push_back(ch);
             }
         }
+        // key table: load factor <= 1/2
+        uint32_t log2 = 4;
+        while ((1u << log2) < 2 * tc.size() && log2 < kMaxKeySlotsLog2) log2++;
+        std::vector<KeySlot> slots(1u << log2);
+        for (KeySlot& k : slots) { k.sig = 0; k.meta = kEmptySlot; k.key_off = 0; }
+        for (size_t i = 0; i < trie.size(); i++) {
+            for (uint32_t j = 0; j < tn[i].n_children; j++) {
+                const TrieChild& ch = tc[tn[i].child_begin + j];
+                uint32_t at = key_slot_hash(ch.sig, ch.key_len, (uint32_t)i, log2);
+                while (slots[at].meta != kEmptySlot) at = (at + 1) & ((1u << log2) - 1);
+                slots[at].sig = ch.sig;
+                slots[at].meta = ch.key_len | ((uint32_t)i << 16) | (ch.node << 24);
+                slots[at].key_off = ch.key_off;
+            }
+        }
+        hdr.key_slots_log2 = log2;
         hdr.n_trie_nodes = (uint32_t)tn.size();
         hdr.off_trie_nodes = (uint32_t)b.align16();
         b.append(tn.data(), tn.size() * sizeof(TrieNode));
         hdr.off_trie_children = (uint32_t)b.align16();
         b.append(tc.data(), tc.size() * sizeof(TrieChild));
+        hdr.off_key_slots = (uint32_t)b.align16();
+        b.append(slots.data(), slots.size() * sizeof(KeySlot));
         std::vector<SelectorPatterns> sp(sels.size());
         std::vector<uint16_t> plist;
         for (size_t s = 0; s < sels.size(); s++) {

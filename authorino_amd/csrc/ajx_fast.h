@@ -63,6 +63,8 @@ struct Block16 {
 struct Scan {
     const TrieNode* tn;
     const TrieChild* tc;
+    const KeySlot* ks;  // key table (1 << ks_log2 slots)
+    uint32_t ks_log2;
     const uint8_t* lits;
     const uint8_t* d;
     uint64_t* row;  // capture row (header + records)
@@ -73,6 +75,9 @@ struct Scan {
     int32_t bpos;       // doc position of the current block's byte 0
     uint32_t mbs;       // backslash bits of the current block
     uint32_t carry_bs;  // last backslash before the current block (~0u none)
+    uint32_t oq;        // opening-quote bits of the current block
+    uint32_t carry_oq;  // last opening quote before the current block
+    uint32_t last_oq;
 
     uint64_t is_arr;    // bit k: container at depth k (1-based) is an array
     uint64_t nodes_lo;  // trie node per depth 1..8 (kNoNode = none)
@@ -102,6 +107,11 @@ struct Scan {
     AJX_HD uint32_t byte_at(uint32_t i) const {
         const uint64_t v0 = cl >> ((i & 7u) * 8), v1 = chh >> ((i & 7u) * 8);
         return (uint32_t)(i < 8 ? v0 : v1) & 0xFFu;
+    }
+    // opening quote of the string whose closing quote is at current-block offset i
+    AJX_HD uint32_t open_before(uint32_t i) const {
+        const uint32_t ob = oq & ((1u << i) - 1u);
+        return ob ? (uint32_t)(bpos + (int32_t)hibit32(ob)) : carry_oq;
     }
     AJX_HD uint32_t last_bs_before(uint32_t i) const {
         const uint32_t mb = mbs & ((1u << i) - 1u);
@@ -256,26 +266,29 @@ struct Scan {
         pending = kNoNode;
         const uint32_t parent = node_at(depth);
         if (parent == kNoNode) return;
-        const uint32_t nc = tn[parent].n_children;
-        if (!nc) return;
+        // (a live node always has children: open_container stores only those)
         const uint32_t lb = last_bs_before(i);
         if (lb != ~0u && lb > str_open) { st = X_SLOW; return; }  // escaped key on a live path
-        const uint32_t ks = str_open + 1, klen = p - ks;
+        const uint32_t k0 = str_open + 1, klen = p - k0;
         uint64_t sig = tail8(i);
         if (klen < 8) sig = klen ? sig >> (8 * (8 - klen)) : 0ull;
-        const uint32_t cb = tn[parent].child_begin;
-        for (uint32_t c = 0; c < nc; c++) {
-            const TrieChild* ch = tc + cb + c;
-            if (ch->sig != sig || ch->key_len != klen) continue;
+        const uint32_t want = (klen & 0xFFFFu) | (parent << 16), mask = (1u << ks_log2) - 1u;
+        uint32_t at = key_slot_hash(sig, klen, parent, ks_log2);
+        for (uint32_t probe = 0; probe <= mask; probe++, at = (at + 1) & mask) {
+            const KeySlot slot = ks[at];
+            if (slot.meta == kEmptySlot) return;
+            if (slot.sig != sig || (slot.meta & 0xFFFFFFu) != want || klen > 0xFFFFu) continue;
             bool eq = true;
-            const uint8_t* kl = lits + ch->key_off;
+            const uint8_t* kl = lits + slot.key_off;
             for (uint32_t k = 0; k + 8 < klen; k++)
-                if (d[ks + k] != kl[k]) { eq = false; break; }
-            if (eq) { pending = ch->node; return; }
+                if (d[k0 + k] != kl[k]) { eq = false; break; }
+            if (eq) { pending = slot.meta >> 24; return; }
         }
     }
 
-    // one token at block offset i (byte c)
+    // one token at block offset i (byte c). Strings arrive as one token, their closing
+    // quote (nothing inside a string is a token, so the state before the opening quote
+    // still holds there).
     AJX_HD void token(uint32_t c, uint32_t i) {
         const uint32_t p = (uint32_t)(bpos + (int32_t)i);
         if (gap_cnt) {
@@ -291,20 +304,31 @@ struct Scan {
                 return;
             case X_KEY_OR_CLOSE:
             case X_KEY:
-                if (c == '"') { st = X_IN_KEY; str_open = p; return; }
+                if (c == '"') {
+                    str_open = open_before(i);
+                    st = X_COLON;
+                    key_closed(p, i);
+                    return;
+                }
                 if (c == '}' && st == X_KEY_OR_CLOSE) { close_container(p); return; }
                 st = X_SLOW;
-                return;
-            case X_IN_KEY:  // c is the closing quote
-                st = X_COLON;
-                key_closed(p, i);
                 return;
             case X_COLON:
                 st = c == ':' ? X_VALUE : X_SLOW;
                 return;
             case X_VALUE:
             case X_VALUE_OR_CLOSE:
-                if (c == '"') { st = X_IN_VAL; str_open = p; return; }
+                if (c == '"') {
+                    str_open = open_before(i);
+                    const int32_t s = leaf_sel(value_node());
+                    if (s >= 0) {
+                        const uint32_t lb = last_bs_before(i);
+                        record(s, str_open, p + 1, T_STRING, (lb != ~0u && lb > str_open) ? 1u : 0u);
+                    }
+                    element_done();
+                    st = X_COMMA_OR_CLOSE;
+                    return;
+                }
                 if (c == '{' || c == '[') {
                     if (!open_container(c, p)) st = X_SLOW;
                     return;
@@ -312,16 +336,6 @@ struct Scan {
                 if (c == ']' && st == X_VALUE_OR_CLOSE) { close_container(p); return; }
                 st = X_SLOW;
                 return;
-            case X_IN_VAL: {
-                const int32_t s = leaf_sel(value_node());
-                if (s >= 0) {
-                    const uint32_t lb = last_bs_before(i);
-                    record(s, str_open, p + 1, T_STRING, (lb != ~0u && lb > str_open) ? 1u : 0u);
-                }
-                element_done();
-                st = X_COMMA_OR_CLOSE;
-                return;
-            }
             case X_COMMA_OR_CLOSE:
                 if (c == ',') { st = top_is_arr() ? X_VALUE : X_KEY; return; }
                 if ((c == '}' && !top_is_arr()) || (c == ']' && top_is_arr())) { close_container(p); return; }
@@ -384,7 +398,12 @@ struct Scan {
         const uint32_t outside = ~instr & ~qu & valid;
         if (mbs & outside) { st = X_SLOW; return; }  // backslash outside any string
         const uint32_t ns = outside & ~mst & ~mws;    // scalar bytes
-        uint32_t toks = ((mst & outside) | qu) & 0xFFFFu;
+        // tokens: structural bytes outside strings and closing quotes (an opening quote
+        // is the quote after which the string is open)
+        oq = qu & instr;
+        carry_oq = last_oq;
+        if (oq) last_oq = (uint32_t)(bp + (int32_t)hibit32(oq));
+        uint32_t toks = ((mst & outside) | (qu & ~instr)) & 0xFFFFu;
         if constexpr (MODE == 2) {  // ablation: classification only
             gap_cnt += popc32(toks) + popc32(ns);
             return;
@@ -402,6 +421,19 @@ struct Scan {
             below = (2u << i) - 1u;
             token(byte_at(i), i);
             if (st >= X_DONE) return;
+            // compact JSON: the ':' right after a key and the ',' right after a value are
+            // taken in the same iteration
+            const uint32_t nb = i + 1;
+            if ((toks >> nb) & 1u) {
+                const uint32_t c2 = byte_at(nb);
+                const bool colon = st == X_COLON && c2 == ':';
+                const bool comma = st == X_COMMA_OR_CLOSE && c2 == ',';
+                if (colon || comma) {
+                    st = (colon || top_is_arr()) ? X_VALUE : X_KEY;
+                    toks &= ~(1u << nb);
+                    below = (2u << nb) - 1u;
+                }
+            }
         }
         const uint32_t g = ns & ~below & 0xFFFFu;
         if (g) {
@@ -413,17 +445,30 @@ struct Scan {
     }
 };
 
+// the single-pass path's lookup tables of a ruleset (the blob's own, or an LDS copy)
+struct Tables {
+    const TrieNode* tn;
+    const TrieChild* tc;
+    const KeySlot* ks;
+};
+AJX_HD Tables blob_tables(const uint8_t* blob) {
+    const RulesetHdr* h = (const RulesetHdr*)blob;
+    return Tables{(const TrieNode*)(blob + h->off_trie_nodes), (const TrieChild*)(blob + h->off_trie_children),
+                  (const KeySlot*)(blob + h->off_key_slots)};
+}
+
 // Stage A for one request. `row` = capture row (1 + n_selectors u64). Returns true
-// when the row is valid (false: the request needs the exact scan). `tn`/`tc` are the
-// ruleset's trie tables (an LDS copy or the blob's own).
+// when the row is valid (false: the request needs the exact scan).
 // MODE (profiling ablations only): 0 = full scan, 1 = loads only, 2 = loads + classification
 template <int MODE = 0, class LoadBlock>
-AJX_HD bool scan_doc(const uint8_t* blob, const TrieNode* tn, const TrieChild* tc, const uint8_t* d, uint32_t n,
-                     uint64_t* row, LoadBlock load) {
+AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, uint32_t n, uint64_t* row,
+                     LoadBlock load) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
     Scan s;
-    s.tn = tn;
-    s.tc = tc;
+    s.tn = tab.tn;
+    s.tc = tab.tc;
+    s.ks = tab.ks;
+    s.ks_log2 = h->key_slots_log2;
     s.lits = blob + h->off_literals;
     s.d = d;
     s.row = row;
@@ -432,6 +477,8 @@ AJX_HD bool scan_doc(const uint8_t* blob, const TrieNode* tn, const TrieChild* t
     s.bpos = 0;
     s.mbs = 0;
     s.carry_bs = ~0u;
+    s.oq = 0;
+    s.carry_oq = s.last_oq = 0;
     s.is_arr = 0;
     s.nodes_lo = s.nodes_hi = ~0ull;
     s.found = 0;
@@ -488,9 +535,7 @@ AJX_HD bool scan_doc(const uint8_t* blob, const TrieNode* tn, const TrieChild* t
 
 template <int MODE = 0, class LoadBlock>
 AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t* row, LoadBlock load) {
-    const RulesetHdr* h = (const RulesetHdr*)blob;
-    return scan_doc<MODE>(blob, (const TrieNode*)(blob + h->off_trie_nodes),
-                          (const TrieChild*)(blob + h->off_trie_children), d, n, row, load);
+    return scan_doc<MODE>(blob, blob_tables(blob), d, n, row, load);
 }
 
 // Stage B for one request: patterns on the captured values, bitmap, fold.

@@ -109,6 +109,40 @@ __global__ __launch_bounds__(256) void ajx_eval_scan_list(const uint8_t* const* 
         eval_scan_one(slow_ids[i], sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride);
 }
 
+// LDS image of a ruleset's single-pass tables (SHARED kernels): trie nodes, trie
+// children, key slots, each region sized for the compile limits.
+constexpr uint32_t kLdsNodeWords = kFastMaxNodes * sizeof(TrieNode) / 4;
+constexpr uint32_t kLdsChildWords = kFastMaxNodes * sizeof(TrieChild) / 4;
+constexpr uint32_t kLdsSlotWords = (1u << kMaxKeySlotsLog2) * sizeof(KeySlot) / 4;
+constexpr uint32_t kLdsTabWords = kLdsNodeWords + kLdsChildWords + kLdsSlotWords;
+static_assert((kLdsNodeWords * 4) % 8 == 0 && ((kLdsNodeWords + kLdsChildWords) * 4) % 8 == 0, "LDS table alignment");
+
+// SHARED: the whole batch uses one ruleset; its tables are copied to LDS once per
+// workgroup (every thread reaches the barrier) and the scan reads them with ds_read.
+template <bool SHARED>
+__device__ __forceinline__ Tables stage_tables(const uint8_t* blob, uint32_t* s_tab, bool fast_ok) {
+    Tables t = blob_tables(blob);
+    if constexpr (SHARED) {
+        const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+        if (fast_ok) {  // uniform over the workgroup
+            const uint32_t nn = h->n_trie_nodes;
+            const uint32_t wn = nn * (sizeof(TrieNode) / 4), wc = (nn - 1) * (sizeof(TrieChild) / 4);
+            const uint32_t wk = (1u << h->key_slots_log2) * (sizeof(KeySlot) / 4);
+            const uint32_t* gn = reinterpret_cast<const uint32_t*>(t.tn);
+            const uint32_t* gc = reinterpret_cast<const uint32_t*>(t.tc);
+            const uint32_t* gk = reinterpret_cast<const uint32_t*>(t.ks);
+            for (uint32_t i = threadIdx.x; i < wn; i += blockDim.x) s_tab[i] = gn[i];
+            for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) s_tab[kLdsNodeWords + i] = gc[i];
+            for (uint32_t i = threadIdx.x; i < wk; i += blockDim.x) s_tab[kLdsNodeWords + kLdsChildWords + i] = gk[i];
+        }
+        __syncthreads();
+        t.tn = reinterpret_cast<const TrieNode*>(s_tab);  // unconditionally LDS: ds_read in the scan
+        t.tc = reinterpret_cast<const TrieChild*>(s_tab + kLdsNodeWords);
+        t.ks = reinterpret_cast<const KeySlot*>(s_tab + kLdsNodeWords + kLdsChildWords);
+    }
+    return t;
+}
+
 // Stage A: structural scan -> capture rows (requests it can not handle -> slow list).
 // SHARED: the whole batch uses sets[0]; its trie tables are copied to LDS once per
 // workgroup so the token loop never touches global memory for them.
@@ -121,26 +155,12 @@ __global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __res
                                                      uint64_t* __restrict__ rows, uint32_t row_stride,
                                                      uint32_t* __restrict__ slow_count,
                                                      uint32_t* __restrict__ slow_ids) {
-    __shared__ uint32_t s_tab[SHARED ? (kFastMaxNodes * (sizeof(TrieNode) + sizeof(TrieChild))) / 4 : 1];
+    __shared__ uint32_t s_tab[SHARED ? kLdsTabWords : 1];
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     const uint8_t* blob = sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)];
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    const TrieNode* tn = reinterpret_cast<const TrieNode*>(blob + h->off_trie_nodes);
-    const TrieChild* tc = reinterpret_cast<const TrieChild*>(blob + h->off_trie_children);
     const bool fast_ok = (h->flags & kFlagFastOk) != 0;
-    if constexpr (SHARED) {
-        if (fast_ok) {  // uniform over the workgroup
-            const uint32_t nn = h->n_trie_nodes;
-            const uint32_t wn = nn * (sizeof(TrieNode) / 4), wc = (nn - 1) * (sizeof(TrieChild) / 4);
-            const uint32_t* gn = reinterpret_cast<const uint32_t*>(tn);
-            const uint32_t* gc = reinterpret_cast<const uint32_t*>(tc);
-            for (uint32_t i = threadIdx.x; i < wn; i += blockDim.x) s_tab[i] = gn[i];
-            for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) s_tab[kFastMaxNodes * 2 + i] = gc[i];
-        }
-        __syncthreads();
-        tn = reinterpret_cast<const TrieNode*>(s_tab);  // unconditionally LDS: ds_read in the scan
-        tc = reinterpret_cast<const TrieChild*>(s_tab + kFastMaxNodes * 2);
-    }
+    const Tables tab = stage_tables<SHARED>(blob, s_tab, fast_ok);
     if (r >= n) return;
     uint64_t* row = rows + (size_t)r * row_stride;
     const uint8_t* d = arena + offs[r];
@@ -148,7 +168,7 @@ __global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __res
     bool ok = false;
     if (fast_ok && len < (1u << 24)) {
         const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-        ok = scan_doc<MODE>(blob, tn, tc, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
+        ok = scan_doc<MODE>(blob, tab, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
             if (b < nblk) {
                 const uint4 v = a4[b];
                 return Block16{v.x, v.y, v.z, v.w};
@@ -174,26 +194,12 @@ __global__ __launch_bounds__(256) void ajx_scan_fused(const uint8_t* const* __re
                                                       uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
                                                       int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
                                                       uint32_t stride) {
-    __shared__ uint32_t s_tab[SHARED ? (kFastMaxNodes * (sizeof(TrieNode) + sizeof(TrieChild))) / 4 : 1];
+    __shared__ uint32_t s_tab[SHARED ? kLdsTabWords : 1];
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     const uint8_t* blob = sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)];
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    const TrieNode* tn = reinterpret_cast<const TrieNode*>(blob + h->off_trie_nodes);
-    const TrieChild* tc = reinterpret_cast<const TrieChild*>(blob + h->off_trie_children);
     const bool fast_ok = (h->flags & kFlagFastOk) != 0;
-    if constexpr (SHARED) {
-        if (fast_ok) {
-            const uint32_t nn = h->n_trie_nodes;
-            const uint32_t wn = nn * (sizeof(TrieNode) / 4), wc = (nn - 1) * (sizeof(TrieChild) / 4);
-            const uint32_t* gn = reinterpret_cast<const uint32_t*>(tn);
-            const uint32_t* gc = reinterpret_cast<const uint32_t*>(tc);
-            for (uint32_t i = threadIdx.x; i < wn; i += blockDim.x) s_tab[i] = gn[i];
-            for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) s_tab[kFastMaxNodes * 2 + i] = gc[i];
-        }
-        __syncthreads();
-        tn = reinterpret_cast<const TrieNode*>(s_tab);
-        tc = reinterpret_cast<const TrieChild*>(s_tab + kFastMaxNodes * 2);
-    }
+    const Tables tab = stage_tables<SHARED>(blob, s_tab, fast_ok);
     if (r >= n) return;
     uint64_t* row = rows + (size_t)r * row_stride;
     const uint8_t* d = arena + offs[r];
@@ -201,7 +207,7 @@ __global__ __launch_bounds__(256) void ajx_scan_fused(const uint8_t* const* __re
     bool ok = false;
     if (fast_ok && len < (1u << 24)) {
         const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-        ok = scan_doc<0>(blob, tn, tc, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
+        ok = scan_doc<0>(blob, tab, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
             if (b < nblk) {
                 const uint4 v = a4[b];
                 return Block16{v.x, v.y, v.z, v.w};

@@ -3,7 +3,8 @@ import json
 
 import numpy as np
 
-KEYS = ["a", "b", "c", "ab", "x.y", "0", "1", "ké", "long-key-name", "", "a b", "q\"t", "s\\l", "n"]
+KEYS = ["a", "b", "c", "ab", "x.y", "0", "1", "ké", "long-key-name", "", "a b", "q\"t", "s\\l", "n",
+        "a-long-key-name", "b-long-key-name"]
 STRS = ["", "x", "hello", "a\"b", "back\\slash", "t\tab", "é", "\U0001F600", "<&>", "1", "true", "null",
         "line\nbreak", " ", "-0", "GET", "/api/v1/orders/7"]
 NUMS = ["0", "-0", "1", "-12", "007", "1.5", "1.50", "1e3", "1E-7", "-0.0", "123456789012345", "0.1", "2.5e10",
