@@ -210,9 +210,11 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         HIP_OK(ajx::launch_eval_scan(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
     else
-        HIP_OK(ajx::launch_eval_fast(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
-                                     d_out_err_idx, d_out_bitmap, bitmap_stride_words, ctx->d_rows, row_stride,
-                                     ctx->d_slow, ctx->d_slow + 1, s, ctx->ablate));
+        HIP_OK(ajx::launch_eval_fast(
+            ctx->d_sets, d_set_of_req,
+            (n_sets == 1 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes) ? (uint32_t)sets[0]->c.blob.size() : 0u,
+            d_arena, d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words, ctx->d_rows,
+            row_stride, ctx->d_slow, ctx->d_slow + 1, s, ctx->ablate));
     HIP_OK(hipEventRecord(ctx->ev1, s));
     return AUTHJX_OK;
 }

@@ -375,13 +375,36 @@ AJX_HD bool string_of(const uint8_t* d, const ValueRef& v, StrSrc* s) {
     }
 }
 
+// the 4 bytes at p (any alignment) from the aligned dword(s) holding them; the second
+// dword is read only when a byte lies in it. (Pointer arithmetic, not an integer cast,
+// keeps the address space of an LDS pointer.)
+AJX_HD uint32_t load_u32_any(const uint8_t* p) {
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t* q = (const uint32_t*)(p - sh);
+    const uint32_t w0 = q[0];
+    const uint32_t w1 = sh ? q[1] : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbyte(w1, w0, sh);
+#else
+    return sh ? (w0 >> (8 * sh)) | (w1 << (32 - 8 * sh)) : w0;
+#endif
+}
+
+// a[0..len) == b[0..len), a dword at a time
+AJX_HD bool bytes_equal(const uint8_t* a, const uint8_t* b, uint32_t len) {
+    uint32_t k = 0;
+    for (; k + 4 <= len; k += 4)
+        if (load_u32_any(a + k) != load_u32_any(b + k)) return false;
+    for (; k < len; k++)
+        if (a[k] != b[k]) return false;
+    return true;
+}
+
 // stream == literal ?
 AJX_HD bool stream_equals(StrSrc* s, const uint8_t* lit, uint32_t len) {
     if (s->kind == StrSrc::S_RAW) {
         if (s->n - s->i != len) return false;
-        for (uint32_t k = 0; k < len; k++)
-            if (s->p[s->i + k] != lit[k]) return false;
-        return true;
+        return bytes_equal(s->p + s->i, lit, len);
     }
     for (uint32_t k = 0; k < len; k++) {
         int c = s->next();
@@ -680,6 +703,57 @@ AJX_HD bool dfa_match(const uint8_t* blob, uint32_t dfa_off, StrSrc* s) {
     const uint8_t* eot = blob + h->eot_off;
     uint32_t st = h->start;
     if (st == h->match_state) return true;
+    const uint32_t nc = h->n_classes, ms = h->match_state;
+    if (s->kind == StrSrc::S_RAW) {  // contiguous bytes: ASCII four at a time, utf8.DecodeRune otherwise
+        const uint8_t* p = s->p;
+        uint32_t i = s->i;
+        const uint32_t n = s->n;
+        while (i < n) {
+            if (i + 4 <= n) {
+                const uint32_t w = load_u32_any(p + i);
+                if (!(w & 0x80808080u)) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        st = tr[st * nc + h->ascii_class[(w >> (8 * k)) & 0x7Fu]];
+                        if (st == ms) return true;
+                    }
+                    i += 4;
+                    continue;
+                }
+            }
+            const uint32_t b0 = p[i];
+            int32_t r = (int32_t)b0;
+            uint32_t sz = 1;
+            if (b0 >= 0x80) {
+                r = 0xFFFD;
+                uint32_t need = 0, lo = 0x80, hi = 0xBF, v = 0;
+                if (b0 >= 0xC2 && b0 <= 0xDF) { need = 2; v = b0 & 0x1F; }
+                else if (b0 >= 0xE0 && b0 <= 0xEF) {
+                    need = 3; v = b0 & 0x0F;
+                    if (b0 == 0xE0) lo = 0xA0;
+                    if (b0 == 0xED) hi = 0x9F;
+                } else if (b0 >= 0xF0 && b0 <= 0xF4) {
+                    need = 4; v = b0 & 0x07;
+                    if (b0 == 0xF0) lo = 0x90;
+                    if (b0 == 0xF4) hi = 0x8F;
+                }
+                if (need && n - i >= need && p[i + 1] >= lo && p[i + 1] <= hi) {
+                    bool good = true;
+                    v = (v << 6) | (p[i + 1] & 0x3Fu);
+                    for (uint32_t k = 2; k < need; k++) {
+                        const uint32_t c = p[i + k];
+                        if (c < 0x80 || c > 0xBF) { good = false; break; }
+                        v = (v << 6) | (c & 0x3Fu);
+                    }
+                    if (good) { r = (int32_t)v; sz = need; }
+                }
+            }
+            i += sz;
+            st = tr[st * nc + rune_class(h, blob, r)];
+            if (st == ms) return true;
+        }
+        return eot[st] != 0;
+    }
     RuneReader rd;
     rd.init(s);
     for (;;) {
@@ -775,6 +849,64 @@ AJX_HD uint8_t run_fold(const uint32_t* code, uint32_t n_code, ResFn res, int32_
     }
     *err = (out == V_E || out == V_U) ? out_ep : -1;
     return out;
+}
+
+// run_fold for rulesets of at most 128 patterns whose results are bitmaps (T, undecided,
+// static E): the same evaluation with the stack packed into registers — kind 1 bit,
+// value 2 bits, error pattern + 1 in 8 bits per level — instead of indexed arrays
+// (which would live in scratch memory).
+AJX_HD uint64_t sel64(bool c, uint64_t a, uint64_t b) { return c ? a : b; }  // a value select
+
+AJX_HD uint8_t run_fold_bits(const uint32_t* code, uint32_t n_code, const uint64_t t[2], const uint64_t u[2],
+                             const uint64_t se[2], int32_t* err) {
+    const uint64_t t0 = t[0], t1 = t[1], u0 = u[0], u1 = u[1], s0 = se[0], s1 = se[1];
+    uint32_t kinds = 0, vals = 0;
+    uint64_t ep_lo = 0, ep_hi = 0;  // levels 0..7 / 8..15
+    uint32_t sp = 0;
+    uint32_t out = V_T, out_e = 0;
+    for (uint32_t k = 0; k < n_code; k++) {
+        const uint32_t w = code[k];
+        const uint32_t op = w >> 24, arg = w & 0xFFFFFFu;
+        uint32_t v = V_T, e = 0;
+        if (op == C_OPEN_AND || op == C_OPEN_OR) {
+            const uint32_t sh = 2 * sp;
+            kinds = (kinds & ~(1u << sp)) | ((op == C_OPEN_OR ? 1u : 0u) << sp);
+            vals = (vals & ~(3u << sh)) | ((op == C_OPEN_OR ? (uint32_t)V_F : (uint32_t)V_T) << sh);
+            const uint64_t m = ~(0xFFull << ((sp & 7) * 8));
+            ep_lo = sel64(sp < 8, ep_lo & m, ep_lo);
+            ep_hi = sel64(sp < 8, ep_hi, ep_hi & m);
+            sp++;
+            continue;
+        }
+        if (op == C_CONST_F) v = V_F;
+        if (op == C_PAT) {
+            const uint64_t bit = 1ull << (arg & 63);
+            const uint32_t q = arg >> 6;
+            const uint64_t tq = sel64(q != 0, t1, t0), uq = sel64(q != 0, u1, u0), sq = sel64(q != 0, s1, s0);
+            v = (sq & bit) ? V_E : (uq & bit) ? V_U : (tq & bit) ? V_T : V_F;
+            e = (v == V_E || v == V_U) ? arg + 1 : 0u;
+        }
+        if (op == C_CLOSE) {
+            sp--;
+            v = (vals >> (2 * sp)) & 3u;
+            e = (uint32_t)((sel64(sp < 8, ep_lo, ep_hi) >> ((sp & 7) * 8)) & 0xFFu);
+        }
+        if (sp == 0) {
+            out = v;
+            out_e = e;
+        } else {
+            const uint32_t top = sp - 1;
+            const uint32_t ident = ((kinds >> top) & 1u) ? (uint32_t)V_F : (uint32_t)V_T;
+            if (((vals >> (2 * top)) & 3u) == ident) {
+                vals = (vals & ~(3u << (2 * top))) | (v << (2 * top));
+                const uint64_t m = 0xFFull << ((top & 7) * 8), x = (uint64_t)e << ((top & 7) * 8);
+                ep_lo = sel64(top < 8, (ep_lo & ~m) | x, ep_lo);
+                ep_hi = sel64(top < 8, ep_hi, (ep_hi & ~m) | x);
+            }
+        }
+    }
+    *err = (out == V_E || out == V_U) ? (int32_t)out_e - 1 : -1;
+    return (uint8_t)out;
 }
 
 }  // namespace ajx

@@ -542,32 +542,67 @@ AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t
 // res(p) values are V_T / V_F / V_E / V_U.
 AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, const uint64_t* row, uint64_t t[2],
                               uint64_t u[2]) {
+    // selector by selector: each captured value is decoded once for all its patterns;
+    // when its String() is a contiguous byte span (unescaped string, integer, literal,
+    // raw JSON) eq/neq compare a dword at a time and `matches` runs the DFA straight
+    // over the span
     const RulesetHdr* h = (const RulesetHdr*)blob;
     const Pattern* pats = (const Pattern*)(blob + h->off_patterns);
+    const SelectorPatterns* sps = (const SelectorPatterns*)(blob + h->off_sel_patterns);
+    const uint16_t* plist = (const uint16_t*)(blob + h->off_pattern_lists);
+    const uint8_t* lits = blob + h->off_literals;
     const uint64_t found = row[0];
-    t[0] = t[1] = 0;
-    u[0] = h->unsupported[0];
-    u[1] = h->unsupported[1];
-    for (uint32_t p = 0; p < h->n_patterns; p++) {
-        const Pattern pt = pats[p];
-        if (pt.state != P_OK) continue;
-        const uint64_t bit = 1ull << (p & 63);
-        ValueRef v;
-        if ((found >> pt.selector) & 1) {
-            const uint64_t rec = row[1 + pt.selector];
-            const uint32_t meta = (uint32_t)(rec >> 32);
-            v.start = (uint32_t)rec;
-            v.end = v.start + (meta & 0xFFFFFFu);
-            v.type = (uint8_t)((meta >> 24) & 7u);
-            v.esc = (uint8_t)((meta >> 27) & 1u);
-        } else {
-            if (h->null_true[p >> 6] & bit) t[p >> 6] |= bit;
+    uint64_t t0 = 0, t1 = 0, u0 = h->unsupported[0], u1 = h->unsupported[1];
+    const uint64_t nt0 = h->null_true[0], nt1 = h->null_true[1];
+    const uint32_t ns = h->n_selectors;
+    for (uint32_t s = 0; s < ns; s++) {
+        const uint32_t cnt = sps[s].count;
+        if (!cnt) continue;
+        if (!((found >> s) & 1)) {  // Null result
+            t0 |= sps[s].mask[0] & nt0;
+            t1 |= sps[s].mask[1] & nt1;
             continue;
         }
-        const uint8_t r = eval_pattern(blob, pt, doc, v);
-        if (r == V_T) t[p >> 6] |= bit;
-        else if (r == V_U) u[p >> 6] |= bit;
+        const uint64_t rec = row[1 + s];
+        const uint32_t meta = (uint32_t)(rec >> 32);
+        ValueRef v;
+        v.start = (uint32_t)rec;
+        v.end = v.start + (meta & 0xFFFFFFu);
+        v.type = (uint8_t)((meta >> 24) & 7u);
+        v.esc = (uint8_t)((meta >> 27) & 1u);
+        StrSrc base;
+        const bool raw = string_of(doc, v, &base) && base.kind == StrSrc::S_RAW;
+        const uint8_t* rp = raw ? base.p + base.i : doc;
+        const uint32_t rn = raw ? base.n - base.i : 0u;
+        const uint32_t begin = sps[s].begin;
+        for (uint32_t j = 0; j < cnt; j++) {
+            const uint32_t p = plist[begin + j];
+            const Pattern pt = pats[p];
+            uint8_t r;
+            if (raw && (pt.op == OP_EQ || pt.op == OP_NEQ)) {
+                const bool eq = rn == pt.lit_len && bytes_equal(rp, lits + pt.lit_off, rn);
+                r = eq == (pt.op == OP_EQ) ? V_T : V_F;
+            } else if (raw && pt.op == OP_MATCHES) {
+                StrSrc sc;
+                sc.init_raw(rp, 0, rn);
+                r = dfa_match(blob, pt.dfa_off, &sc) ? V_T : V_F;
+            } else {
+                r = eval_pattern(blob, pt, doc, v);
+            }
+            const uint64_t bit = 1ull << (p & 63);
+            if (r == V_T) {
+                if (p < 64) t0 |= bit;
+                else t1 |= bit;
+            } else if (r == V_U) {
+                if (p < 64) u0 |= bit;
+                else u1 |= bit;
+            }
+        }
     }
+    t[0] = t0;
+    t[1] = t1;
+    u[0] = u0;
+    u[1] = u1;
 }
 
 }  // namespace ajx

@@ -13,11 +13,18 @@ hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_
 
 namespace ajx {
 
-// single-pass fast kernel + exact scan of the requests it hands over (d_slow_count is
-// zeroed on the stream first; d_slow_ids needs room for n entries)
-hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
-                            const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
-                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows, uint32_t row_stride,
-                            uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream, int ablate = 0);
+// Largest ruleset blob the kernels stage into LDS (a batch over one ruleset).
+constexpr uint32_t kMaxSharedBlobBytes = 48 * 1024;
+
+// single-pass kernel + exact scan of the requests it hands over (d_slow_count is zeroed
+// on the stream first; d_slow_ids needs room for n entries). shared_blob_bytes: the
+// blob size of sets[0] when every request uses it and it fits kMaxSharedBlobBytes,
+// else 0. mode (profiling only): 0 fused single pass, 1 stage-A loads only, 2 stage-A
+// loads + classification, 3 stage A and stage B as separate launches.
+hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
+                            const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                            uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
+                            uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
+                            int mode = 0);
 
 }  // namespace ajx

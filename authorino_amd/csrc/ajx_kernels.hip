@@ -109,43 +109,65 @@ __global__ __launch_bounds__(256) void ajx_eval_scan_list(const uint8_t* const* 
         eval_scan_one(slow_ids[i], sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride);
 }
 
-// LDS image of a ruleset's single-pass tables (SHARED kernels): trie nodes, trie
-// children, key slots, each region sized for the compile limits.
-constexpr uint32_t kLdsNodeWords = kFastMaxNodes * sizeof(TrieNode) / 4;
-constexpr uint32_t kLdsChildWords = kFastMaxNodes * sizeof(TrieChild) / 4;
-constexpr uint32_t kLdsSlotWords = (1u << kMaxKeySlotsLog2) * sizeof(KeySlot) / 4;
-constexpr uint32_t kLdsTabWords = kLdsNodeWords + kLdsChildWords + kLdsSlotWords;
-static_assert((kLdsNodeWords * 4) % 8 == 0 && ((kLdsNodeWords + kLdsChildWords) * 4) % 8 == 0, "LDS table alignment");
-
-// SHARED: the whole batch uses one ruleset; its tables are copied to LDS once per
-// workgroup (every thread reaches the barrier) and the scan reads them with ds_read.
+// SHARED kernels: the whole batch uses sets[0], and the ruleset blob (trie, key table,
+// patterns, literals, DFA tables, fold code — h->total_bytes, a multiple of 16) is
+// copied into dynamic LDS once per workgroup; every thread reaches the barrier. All
+// table reads of the scan and the patterns are then ds_reads.
 template <bool SHARED>
-__device__ __forceinline__ Tables stage_tables(const uint8_t* blob, uint32_t* s_tab, bool fast_ok) {
-    Tables t = blob_tables(blob);
+__device__ __forceinline__ const uint8_t* stage_blob(const uint8_t* gblob) {
     if constexpr (SHARED) {
-        const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-        if (fast_ok) {  // uniform over the workgroup
-            const uint32_t nn = h->n_trie_nodes;
-            const uint32_t wn = nn * (sizeof(TrieNode) / 4), wc = (nn - 1) * (sizeof(TrieChild) / 4);
-            const uint32_t wk = (1u << h->key_slots_log2) * (sizeof(KeySlot) / 4);
-            const uint32_t* gn = reinterpret_cast<const uint32_t*>(t.tn);
-            const uint32_t* gc = reinterpret_cast<const uint32_t*>(t.tc);
-            const uint32_t* gk = reinterpret_cast<const uint32_t*>(t.ks);
-            for (uint32_t i = threadIdx.x; i < wn; i += blockDim.x) s_tab[i] = gn[i];
-            for (uint32_t i = threadIdx.x; i < wc; i += blockDim.x) s_tab[kLdsNodeWords + i] = gc[i];
-            for (uint32_t i = threadIdx.x; i < wk; i += blockDim.x) s_tab[kLdsNodeWords + kLdsChildWords + i] = gk[i];
-        }
+        extern __shared__ uint4 s_blob[];
+        const uint32_t nq = reinterpret_cast<const RulesetHdr*>(gblob)->total_bytes / 16;
+        const uint4* g = reinterpret_cast<const uint4*>(gblob);
+        for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) s_blob[i] = g[i];
         __syncthreads();
-        t.tn = reinterpret_cast<const TrieNode*>(s_tab);  // unconditionally LDS: ds_read in the scan
-        t.tc = reinterpret_cast<const TrieChild*>(s_tab + kLdsNodeWords);
-        t.ks = reinterpret_cast<const KeySlot*>(s_tab + kLdsNodeWords + kLdsChildWords);
+        return reinterpret_cast<const uint8_t*>(s_blob);
+    } else {
+        return gblob;
     }
-    return t;
 }
 
-// Stage A: structural scan -> capture rows (requests it can not handle -> slow list).
-// SHARED: the whole batch uses sets[0]; its trie tables are copied to LDS once per
-// workgroup so the token loop never touches global memory for them.
+// stage A for request r: single-pass scan into its capture row (false: slow list)
+template <int MODE>
+__device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t* d, uint32_t len, uint64_t* row) {
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    if (!(h->flags & kFlagFastOk) || len >= (1u << 24)) {
+        row[0] = kRowSlow;
+        return false;
+    }
+    const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
+    return scan_doc<MODE>(blob, blob_tables(blob), d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
+        if (b < nblk) {
+            const uint4 v = a4[b];
+            return Block16{v.x, v.y, v.z, v.w};
+        }
+        return Block16{0u, 0u, 0u, 0u};
+    });
+}
+
+// stage B for request r on its capture row: patterns, T bitmap, And/Or fold, outputs
+__device__ __forceinline__ void finish_request(uint32_t r, const uint8_t* blob, const uint8_t* d, const uint64_t* row,
+                                               uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                               uint64_t* __restrict__ out_bm, uint32_t stride) {
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    uint64_t t[2], u[2];
+    patterns_from_row(blob, d, row, t, u);
+    if (out_bm) {
+        uint64_t* orow = out_bm + (size_t)r * stride;
+        orow[0] = t[0];
+        if (stride > 1) orow[1] = t[1];
+        for (uint32_t w = 2; w < stride; w++) orow[w] = 0ull;
+    }
+    const uint64_t se[2] = {h->static_error[0], h->static_error[1]};
+    int32_t ep;
+    const uint8_t tri =
+        run_fold_bits(reinterpret_cast<const uint32_t*>(blob + h->off_code), h->n_code, t, u, se, &ep);
+    out_tri[r] = tri;
+    if (out_err) out_err[r] = ep;
+}
+
+// Stage A alone (profiling split / ablations): structural scan -> capture rows.
+// MODE 1/2 are the loads-only / loads+classification ablations.
 template <int MODE, bool SHARED>
 __global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
                                                      const uint32_t* __restrict__ set_of_req,
@@ -155,34 +177,33 @@ __global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __res
                                                      uint64_t* __restrict__ rows, uint32_t row_stride,
                                                      uint32_t* __restrict__ slow_count,
                                                      uint32_t* __restrict__ slow_ids) {
-    __shared__ uint32_t s_tab[SHARED ? kLdsTabWords : 1];
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint8_t* blob = sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)];
-    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    const bool fast_ok = (h->flags & kFlagFastOk) != 0;
-    const Tables tab = stage_tables<SHARED>(blob, s_tab, fast_ok);
+    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)]);
     if (r >= n) return;
-    uint64_t* row = rows + (size_t)r * row_stride;
-    const uint8_t* d = arena + offs[r];
-    const uint32_t len = lens[r];
-    bool ok = false;
-    if (fast_ok && len < (1u << 24)) {
-        const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-        ok = scan_doc<MODE>(blob, tab, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
-            if (b < nblk) {
-                const uint4 v = a4[b];
-                return Block16{v.x, v.y, v.z, v.w};
-            }
-            return Block16{0u, 0u, 0u, 0u};
-        });
-    } else {
-        row[0] = kRowSlow;
-    }
-    if (!ok) slow_ids[atomicAdd(slow_count, 1u)] = r;
+    if (!scan_request<MODE>(blob, arena + offs[r], lens[r], rows + (size_t)r * row_stride))
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
 }
 
-// Stages A+B fused: the patterns run right after the scan, while the request's value
-// bytes are still in L2 / MALL (stage B alone re-reads them from HBM).
+// Stage B alone (profiling split): patterns on the captured values, bitmap, fold
+template <bool SHARED>
+__global__ __launch_bounds__(256) void ajx_patterns(const uint8_t* const* __restrict__ sets,
+                                                    const uint32_t* __restrict__ set_of_req,
+                                                    const uint8_t* __restrict__ arena,
+                                                    const uint64_t* __restrict__ offs, uint32_t n,
+                                                    const uint64_t* __restrict__ rows, uint32_t row_stride,
+                                                    uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                                    uint64_t* __restrict__ out_bm, uint32_t stride) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)]);
+    if (r >= n) return;
+    const uint64_t* row = rows + (size_t)r * row_stride;
+    if (row[0] & kRowSlow) return;
+    finish_request(r, blob, arena + offs[r], row, out_tri, out_err, out_bm, stride);
+}
+
+// The single-pass path: stage A then stage B in the same work-item, while the
+// request's value bytes are still in cache (a separate stage-B launch re-reads them
+// from HBM). Requests stage A can not prove gjson-equivalent go to the slow list.
 template <bool SHARED>
 __global__ __launch_bounds__(256) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
                                                       const uint32_t* __restrict__ set_of_req,
@@ -194,85 +215,16 @@ __global__ __launch_bounds__(256) void ajx_scan_fused(const uint8_t* const* __re
                                                       uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
                                                       int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
                                                       uint32_t stride) {
-    __shared__ uint32_t s_tab[SHARED ? kLdsTabWords : 1];
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint8_t* blob = sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)];
-    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    const bool fast_ok = (h->flags & kFlagFastOk) != 0;
-    const Tables tab = stage_tables<SHARED>(blob, s_tab, fast_ok);
+    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)]);
     if (r >= n) return;
     uint64_t* row = rows + (size_t)r * row_stride;
     const uint8_t* d = arena + offs[r];
-    const uint32_t len = lens[r];
-    bool ok = false;
-    if (fast_ok && len < (1u << 24)) {
-        const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-        ok = scan_doc<0>(blob, tab, d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
-            if (b < nblk) {
-                const uint4 v = a4[b];
-                return Block16{v.x, v.y, v.z, v.w};
-            }
-            return Block16{0u, 0u, 0u, 0u};
-        });
-    }
-    if (!ok) {
+    if (!scan_request<0>(blob, d, lens[r], row)) {
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
-    uint64_t t[2], u[2];
-    patterns_from_row(blob, d, row, t, u);
-    if (out_bm) {
-        uint64_t* orow = out_bm + (size_t)r * stride;
-        for (uint32_t w = 0; w < stride; w++) orow[w] = w < 2 ? t[w] : 0ull;
-    }
-    const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
-    int32_t ep;
-    const uint8_t tri = run_fold(code, h->n_code,
-                                 [&](uint32_t p) -> uint8_t {
-                                     const uint64_t bit = 1ull << (p & 63);
-                                     const uint32_t k = p >> 6;
-                                     if (h->static_error[k] & bit) return V_E;
-                                     if (u[k] & bit) return V_U;
-                                     return (t[k] & bit) ? V_T : V_F;
-                                 },
-                                 &ep);
-    out_tri[r] = tri;
-    if (out_err) out_err[r] = ep;
-}
-
-// Stage B: patterns on the captured values, T bitmap, And/Or fold
-__global__ __launch_bounds__(256) void ajx_patterns(const uint8_t* const* __restrict__ sets,
-                                                    const uint32_t* __restrict__ set_of_req,
-                                                    const uint8_t* __restrict__ arena,
-                                                    const uint64_t* __restrict__ offs, uint32_t n,
-                                                    const uint64_t* __restrict__ rows, uint32_t row_stride,
-                                                    uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-                                                    uint64_t* __restrict__ out_bm, uint32_t stride) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
-    const uint64_t* row = rows + (size_t)r * row_stride;
-    if (row[0] & kRowSlow) return;
-    const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
-    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    uint64_t t[2], u[2];
-    patterns_from_row(blob, arena + offs[r], row, t, u);
-    if (out_bm) {
-        uint64_t* orow = out_bm + (size_t)r * stride;
-        for (uint32_t w = 0; w < stride; w++) orow[w] = w < 2 ? t[w] : 0ull;
-    }
-    const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
-    int32_t ep;
-    const uint8_t tri = run_fold(code, h->n_code,
-                                 [&](uint32_t p) -> uint8_t {
-                                     const uint64_t bit = 1ull << (p & 63);
-                                     const uint32_t k = p >> 6;
-                                     if (h->static_error[k] & bit) return V_E;
-                                     if (u[k] & bit) return V_U;
-                                     return (t[k] & bit) ? V_T : V_F;
-                                 },
-                                 &ep);
-    out_tri[r] = tri;
-    if (out_err) out_err[r] = ep;
+    finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride);
 }
 
 hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
@@ -286,40 +238,51 @@ hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_
     return hipGetLastError();
 }
 
-hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
-                            const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
-                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows, uint32_t row_stride,
-                            uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream, int ablate) {
+hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
+                            const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                            uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
+                            uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
+                            int mode) {
     if (n == 0) return hipSuccess;
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
+    const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
+    const uint32_t lds = shared ? shared_blob_bytes : 0u;
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    const bool shared = d_set_of_req == nullptr;
-#define AJX_SCAN(M, S)                                                                                      \
-    hipLaunchKernelGGL((ajx_scan_fast<M, S>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, \
-                       d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids)
-    if (ablate == 3 || ablate == 4) {
-    } else if (ablate == 1) AJX_SCAN(1, true);
-    else if (ablate == 2) AJX_SCAN(2, true);
-    else if (shared) AJX_SCAN(0, true);
-    else AJX_SCAN(0, false);
-#undef AJX_SCAN
-    if (ablate == 3 || ablate == 4) {  // fused A+B (4: per-request ruleset table)
-        if (ablate == 3)
-            hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
-                               d_bm, stride);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        const uint32_t sgrid = grid < 2048 ? grid : 2048;
-        hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
-                           d_offs, d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
+    if (mode == 1 || mode == 2) {  // profiling ablations of stage A (uniform ruleset only)
+        if (!shared) return hipErrorInvalidValue;
+        if (mode == 1)
+            hipLaunchKernelGGL((ajx_scan_fast<1, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+        else
+            hipLaunchKernelGGL((ajx_scan_fast<2, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
         return hipGetLastError();
     }
-    if (ablate) return hipGetLastError();  // profiling ablation: stage A only
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(ajx_patterns, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs, n,
-                       d_rows, row_stride, d_tri, d_err, d_bm, stride);
+    if (mode == 3) {  // profiling split: stage A and stage B as two launches
+        if (shared) {
+            hipLaunchKernelGGL((ajx_scan_fast<0, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            hipLaunchKernelGGL((ajx_patterns<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
+        } else {
+            hipLaunchKernelGGL((ajx_scan_fast<0, false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            hipLaunchKernelGGL((ajx_patterns<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
+        }
+    } else if (shared) {
+        hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
+                           stride);
+    } else {
+        hipLaunchKernelGGL((ajx_scan_fused<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
+                           stride);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t sgrid = grid < 2048 ? grid : 2048;
     hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,

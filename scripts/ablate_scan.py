@@ -1,5 +1,5 @@
 """Profiling helper: time stage A of the single-pass path in its ablation variants
-(0 full split path, 1 loads only, 2 loads + classification, 3 fused scan+patterns) on the c2 workload, interleaved
+(0 fused single pass (default), 1 stage-A loads only, 2 stage-A loads + classification, 3 stage A and B as two launches) on the c2 workload, interleaved
 in one process (cdna_hip_programming.md §5.4 rule 24). Prints one JSON line."""
 import ctypes as C
 import json
