@@ -1,0 +1,52 @@
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py into HBM bytes per
+launch of the dominant kernel (written to profiles/pmc_traffic.json, read by bench.py).
+
+  python scripts/pmc_traffic.py <fetch_dir> <write_dir> <workload> <n> [out.json]
+
+FETCH_SIZE / WRITE_SIZE are reported in KiB. MI355X_MICROARCH.md (HBM/rocprofv3 section):
+FETCH_SIZE counts exactly half the bytes of a wide coalesced streaming read on gfx950;
+other access widths are uncalibrated. The dominant kernel reads each document with
+per-lane 16-byte loads (one document per lane), so both the raw value and the doubled
+value are recorded; `hbm_bytes_per_launch` uses the raw FETCH + WRITE sum (the
+conservative, smaller figure) and the note says so.
+"""
+import csv
+import glob
+import json
+import statistics
+import sys
+
+
+def per_launch(d, counter, kernel_sub):
+    vals = []
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel_sub in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals.append(float(r["Counter_Value"]) * 1024.0)
+    return statistics.median(vals) if vals else None, len(vals)
+
+
+def main():
+    fetch_dir, write_dir, workload, n = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    out = sys.argv[5] if len(sys.argv) > 5 else "profiles/pmc_traffic.json"
+    kernel = sys.argv[6] if len(sys.argv) > 6 else "ajx_scan_fused"
+    fb, nf = per_launch(fetch_dir, "FETCH_SIZE", kernel)
+    wb, nw = per_launch(write_dir, "WRITE_SIZE", kernel)
+    res = {
+        "workload": workload,
+        "n": n,
+        "kernel": kernel,
+        "fetch_bytes_per_launch_raw": fb,
+        "write_bytes_per_launch": wb,
+        "launches": [nf, nw],
+        "hbm_bytes_per_launch": (fb or 0) + (wb or 0),
+        "note": "FETCH_SIZE+WRITE_SIZE (KiB*1024), median over launches, raw (not doubled): per-lane 16-B "
+                "loads are outside the guide's calibrated access shapes",
+    }
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
