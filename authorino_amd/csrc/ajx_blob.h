@@ -57,11 +57,13 @@ struct Pattern {
     uint32_t selector;
     uint8_t op;
     uint8_t state;
-    uint16_t pad;
+    uint16_t litf;     // kLit*: the literal equals "true" / "false" / "" (String() of a literal value)
     uint32_t lit_off;
     uint32_t lit_len;
     uint32_t dfa_off;  // byte offset of a DfaHdr in the blob (0 = none)
 };
+
+constexpr uint16_t kLitTrue = 1, kLitFalse = 2, kLitEmpty = 4;
 
 struct DfaHdr {
     uint32_t n_states;
@@ -156,7 +158,7 @@ struct RulesetHdr {
     uint32_t off_literals;
     uint32_t lit_bytes;
     uint32_t n_components;
-    uint32_t flags;  // bit0: has regex; bit1: has unsupported pattern; bit2: fast path ok
+    uint32_t flags;  // bit0: has regex; bit1: has unsupported pattern; bit2: fast path ok; bit3: line engine ok
     uint32_t n_trie_nodes;
     uint32_t off_trie_nodes;
     uint32_t off_trie_children;
@@ -170,5 +172,7 @@ struct RulesetHdr {
     uint64_t unsupported[2];    // pattern p can not be decided on the device
 };
 constexpr uint32_t kFlagFastOk = 4;
+constexpr uint32_t kFlagLinesOk = 8;   // eligible for the line engine (ajx_lines.h)
+constexpr uint32_t kLinesMaxDepth = 8; // selector depth the line engine tracks
 
 }  // namespace ajx

@@ -201,8 +201,10 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
         Pattern& p = pats[i];
         std::memset(&p, 0, sizeof p);
         p.op = (uint8_t)(ap.op >= 0 && ap.op <= 5 ? ap.op : 0);
+        while (lits.size() % 4) lits.push_back('\0');  // dword-aligned literals (line engine compares)
         p.lit_off = (uint32_t)lits.size();
         p.lit_len = (uint32_t)val.size();
+        p.litf = (uint16_t)((val == "true" ? kLitTrue : 0) | (val == "false" ? kLitFalse : 0) | (val.empty() ? kLitEmpty : 0));
         lits += val;
         // Pattern.Matches: the operator decides first whether an error is returned
         if (ap.op < AUTHJX_OP_EQ || ap.op > AUTHJX_OP_MATCHES) {
@@ -313,6 +315,11 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
         if (nt && i < 128) null_true[i >> 6] |= bit;
     }
     if (fast_ok) flags |= kFlagFastOk;
+    // the line engine tracks live containers up to kLinesMaxDepth levels deep
+    bool lines_ok = fast_ok;
+    for (size_t s = 0; s < sels.size(); s++)
+        if (sels[s].comp_count > kLinesMaxDepth) lines_ok = false;
+    if (lines_ok) flags |= kFlagLinesOk;
 
     // ---- assemble ----
     Builder b;
@@ -334,6 +341,7 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
                 const std::string& key = trie[i].keys[j].first;
                 ch.sig = key_signature((const uint8_t*)key.data(), (uint32_t)key.size());
                 ch.key_len = (uint32_t)key.size();
+                while (lits.size() % 4) lits.push_back('\0');
                 ch.key_off = (uint32_t)lits.size();
                 lits += key;
                 ch.array_index = trie[i].keys[j].second;
@@ -393,6 +401,7 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
     hdr.off_code = (uint32_t)b.align16();
     b.append(code.data(), code.size() * sizeof(uint32_t));
     hdr.off_literals = (uint32_t)b.align16();
+    lits.append(16, '\0');  // dword reads past a literal's end stay inside the pool
     b.append(lits.data(), lits.size());
     for (uint32_t i = 0; i < np; i++) {
         if (dfa_of[i] < 0) continue;

@@ -15,6 +15,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libauthjx.so")
+# profiling only: AUTHJX_LIB points the binding at an ablation build of the same C-ABI
+LIB_PATH = os.environ.get("AUTHJX_LIB", LIB_PATH)
 
 OP_UNKNOWN, OP_EQ, OP_NEQ, OP_INCL, OP_EXCL, OP_MATCHES = range(6)
 F, T, E, UNDECIDED = 0, 1, 2, 3
@@ -146,6 +148,13 @@ class Context:
     def set_exact_scan(self, force: bool) -> None:
         """Route every request through the exact scan kernel (for cross-checks)."""
         _check(load_library().authjx_set_exact_scan(self._h, 1 if force else 0), "authjx_set_exact_scan")
+
+    def set_kernel_mode(self, mode: int) -> None:
+        """Select the single-pass kernel variant (0 default, 5 the line engine; others are
+        profiling ablations whose outputs are meaningless). Not part of authjx.h."""
+        L = load_library()
+        L.authjx_debug_ablate.argtypes = [C.c_void_p, C.c_int]
+        _check(L.authjx_debug_ablate(self._h, int(mode)), "authjx_debug_ablate")
 
     def last_exact_count(self) -> int:
         """Requests of the last batch the single-pass kernel handed to the exact scan."""

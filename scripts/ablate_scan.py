@@ -1,6 +1,7 @@
-"""Profiling helper: time stage A of the single-pass path in its ablation variants
-(0 fused single pass (default), 1 stage-A loads only, 2 stage-A loads + classification, 3 stage A and B as two launches) on the c2 workload, interleaved
-in one process (cdna_hip_programming.md §5.4 rule 24). Prints one JSON line."""
+"""Profiling helper: time the fast-path variants interleaved in one process
+(cdna_hip_programming.md §5.4 rule 24) and print one JSON line. Modes (authjx_debug_ablate):
+0 single-pass kernel (default), 5 line engine, 11 line engine loads + ring writes only,
+12 + classification, 1/2 single-pass loads / + classification, 3 stage A / stage B split."""
 import ctypes as C
 import json
 import os
@@ -30,10 +31,11 @@ err = torch.empty(n, dtype=torch.int32, device=dev)
 bm = torch.empty((n, (R + 63) // 64), dtype=torch.int64, device=dev)
 stream = torch.cuda.Stream(dev)
 torch.cuda.set_stream(stream)
-res = {0: [], 1: [], 2: [], 3: []}
+MODES = [int(m) for m in (sys.argv[3].split(',') if len(sys.argv) > 3 else ['0', '5', '11', '12'])]
+res = {m: [] for m in MODES}
 outs = {}
 for rep in range(6):
-    for mode in (0, 1, 2, 3):
+    for mode in MODES:
         L.authjx_debug_ablate(ctx._h, mode)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
@@ -42,9 +44,11 @@ for rep in range(6):
         torch.cuda.synchronize()
         if rep:
             res[mode].append(a.elapsed_time(b))
-        if mode in (0, 3) and rep == 1:
+        if rep == 1 and mode == 0:
+            exact0 = ctx.last_exact_count()
+        if mode in (0, 5) and rep == 1:
             outs[mode] = (tri.cpu().numpy().copy(), bm.cpu().numpy().copy())
 bytes_ = int(w.lens.astype(np.int64).sum())
 out = {m: {"ms": float(np.median(v)), "GBps": bytes_ / (np.median(v) * 1e-3) / 1e9} for m, v in res.items() if v}
-same = bool(np.array_equal(outs[0][0], outs[3][0]) and np.array_equal(outs[0][1], outs[3][1]))
-print(json.dumps({"workload": wl, "n": n, "doc_bytes": bytes_, "modes": out, "fused_equals_split": same}))
+same = bool(np.array_equal(outs[0][0], outs[5][0]) and np.array_equal(outs[0][1], outs[5][1])) if 5 in outs else None
+print(json.dumps({"workload": wl, "n": n, "doc_bytes": bytes_, "exact_requests_mode0": exact0, "modes": out, "lines_equal_fused": same}))
