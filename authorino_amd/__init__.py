@@ -7,10 +7,14 @@ for gfx950 that evaluate micro-batches of Authorization-JSON documents. This Pyt
 package mirrors the reference's Go interfaces on top of that C-ABI:
 
   authorino_amd.jsonexp        pkg/jsonexp/expressions.go   (Pattern, And, Or, All, Any)
-  authorino_amd.authorization  pkg/evaluators/authorization/json.go (JSONPatternMatching)
+  authorino_amd.authorization  pkg/evaluators/authorization/json.go (JSONPatternMatching) and
+                               controllers/auth_config_controller.go:805-852 (CRD -> tree)
   authorino_amd.pipeline       pkg/service/auth_pipeline.go (evaluateConditions, authz phase)
   authorino_amd.runtime        C-ABI binding (ctypes), device context, batch evaluation
+  authorino_amd.workloads      BASELINE configs c1-c3 (synthetic Authorization JSON, Go encoding)
 """
 from . import jsonexp  # noqa: F401
 
-__all__ = ["jsonexp"]
+from . import authorization, pipeline  # noqa: F401,E402
+
+__all__ = ["jsonexp", "authorization", "pipeline"]

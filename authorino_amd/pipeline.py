@@ -1,0 +1,201 @@
+"""Host-side mirror of the parts of pkg/service/auth_pipeline.go that sit on the hot path:
+the `when` gates and the authorization phase, batched over many requests.
+
+  evaluate_conditions              auth_pipeline.go:378-388  (nil -> pass; err -> err;
+                                   false -> "unmatching conditions for config")
+  AuthConfig-level conditions      auth_pipeline.go:454-457  (not met -> OK, skipped)
+  evaluator-level conditions       auth_pipeline.go:120-125  (not met -> evaluator ignored)
+  authorization phase              auth_pipeline.go:287-322  + groupAuthConfigsByPriority
+                                   :184-201: priorities ascending, every config of a
+                                   priority evaluated, the first failure is PERMISSION_DENIED
+                                   (:478-481); a success stores the object under
+                                   auth.authorization.<name> for later priorities (:312).
+
+AuthPipelineBatch compiles every expression once (the reconcile-time compile point,
+controllers/auth_config_controller.go) and evaluates each priority level of a batch in ONE
+device launch: the (request, expression) pairs are a set_of_req batch whose offsets all
+point into the same document arena. Identity / metadata / response phases are out of
+scope; the documents given are GetAuthorizationJSON's output after those
+phases.
+
+Where the reference is nondeterministic the mirror fixes one order: configs of one
+priority run concurrently in Go and the denial reported is whichever goroutine answers
+first; here it is the first failing config in declaration order (the decision itself,
+deny or not, is the same either way).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import jsonexp
+from .authorization import JSONPatternMatching, UnauthorizedError
+
+UNMATCHING_CONDITIONS = "unmatching conditions for config"
+CODE_OK = 0  # rpc.OK
+CODE_PERMISSION_DENIED = 7  # rpc.PERMISSION_DENIED
+
+
+class ConditionsError(Exception):
+    """fmt.Errorf("unmatching conditions for config") (auth_pipeline.go:385)."""
+
+    def __init__(self):
+        super().__init__(UNMATCHING_CONDITIONS)
+
+
+def evaluate_conditions(conditions: Optional[jsonexp.Expression], authorization_json) -> Optional[Exception]:
+    """AuthPipeline.evaluateConditions (auth_pipeline.go:378-388), one document."""
+    if conditions is None:
+        return None
+    match, err = conditions.matches(authorization_json)
+    if err is not None:
+        return err
+    if not match:
+        return ConditionsError()
+    return None
+
+
+@dataclass
+class AuthorizationConfig:
+    """evaluators.AuthorizationConfig with a JSON pattern-matching evaluator
+    (pkg/evaluators/authorization.go; Priority and Conditions from the CRD)."""
+
+    name: str
+    rules: Optional[jsonexp.Expression] = None  # JSONPatternMatching.Rules
+    conditions: Optional[jsonexp.Expression] = None  # `when`
+    priority: int = 0
+
+
+@dataclass
+class AuthConfig:
+    """The slice of auth.AuthConfig the authorization phase reads."""
+
+    conditions: Optional[jsonexp.Expression] = None  # AuthConfig-level `when`
+    authorization: List[AuthorizationConfig] = field(default_factory=list)
+
+
+@dataclass
+class AuthResult:
+    """auth.AuthResult (code / message) plus the authorization objects granted."""
+
+    code: int = CODE_OK
+    message: str = ""
+    skipped: bool = False  # AuthConfig-level conditions not met (auth_pipeline.go:454-457)
+    denied_by: Optional[str] = None
+    authorization: Dict[str, object] = field(default_factory=dict)
+
+
+def _selects_authorization(expr: Optional[jsonexp.Expression]) -> bool:
+    if expr is None:
+        return False
+    pats, _, _ = expr.flatten()
+    return any(p.selector == "auth.authorization" or p.selector.startswith("auth.authorization.") for p in pats)
+
+
+class AuthPipelineBatch:
+    """The `when` gates + authorization phase of AuthPipeline.Evaluate for a batch."""
+
+    def __init__(self, auth_config: AuthConfig, device: int = 0, ctx=None):
+        from . import runtime
+
+        self.config = auth_config
+        self.ctx = ctx if ctx is not None else runtime.context(device)
+        self._rs: Dict[int, object] = {}
+        exprs = [auth_config.conditions] + [e for c in auth_config.authorization for e in (c.conditions, c.rules)]
+        for e in exprs:
+            if e is not None and id(e) not in self._rs:
+                self._rs[id(e)] = self.ctx.compile_expression(e)
+        prios = sorted({c.priority for c in auth_config.authorization})
+        self.levels = [[c for c in auth_config.authorization if c.priority == p] for p in prios]
+        self._needs_regen = any(_selects_authorization(e) for lvl in self.levels[1:] for c in lvl
+                                for e in (c.conditions, c.rules))
+
+    # one launch: expression k of `exprs` on every request in `reqs`
+    def _eval(self, exprs: Sequence[jsonexp.Expression], reqs: np.ndarray, arena, offs, lens):
+        from . import runtime
+
+        sets = [self._rs[id(e)] for e in exprs]
+        k = len(exprs)
+        sor = np.repeat(np.arange(k, dtype=np.uint32), len(reqs))
+        o = np.tile(offs[reqs], k)
+        ln = np.tile(lens[reqs], k)
+        tri, err, _ = self.ctx.eval_host_arena(sets, arena, o, ln, set_of_req=sor, with_bitmap=False)
+        if (tri == runtime.UNDECIDED).any():
+            raise runtime.AuthjxError("device could not decide a document (AUTHJX_UNDECIDED)")
+        return tri.reshape(k, len(reqs)), err.reshape(k, len(reqs)), sets
+
+    def evaluate(self, docs: Sequence, producer: Optional[Callable[[int, Dict[str, object]], bytes]] = None
+                 ) -> List[AuthResult]:
+        """Evaluate the batch. `producer(i, authorization_objs)` rebuilds request i's
+        Authorization JSON (GetAuthorizationJSON, auth_pipeline.go:542-579) once earlier
+        priorities granted objects; it is required only when a later priority selects
+        auth.authorization.*."""
+        from . import runtime
+
+        if self._needs_regen and producer is None:
+            raise ValueError("a later priority selects auth.authorization.*: pass a producer")
+        n = len(docs)
+        results = [AuthResult() for _ in range(n)]
+        docs = [runtime._b(d) for d in docs]
+
+        def pack(ds):
+            lens = np.fromiter((len(d) for d in ds), dtype=np.uint32, count=len(ds))
+            offs = np.zeros(len(ds), dtype=np.uint64)
+            if len(ds):
+                offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+            return np.frombuffer(b"".join(ds) + b"\0", dtype=np.uint8), offs, lens
+
+        arena, offs, lens = pack(docs)
+        live = np.arange(n)
+        # AuthConfig-level `when` (auth_pipeline.go:454-457): not met -> OK, skipped
+        top = self.config.conditions
+        if top is not None and n:
+            tri, _, _ = self._eval([top], live, arena, offs, lens)
+            met = tri[0] == runtime.T
+            for i in live[~met]:
+                results[i].skipped = True
+            live = live[met]
+        for li, level in enumerate(self.levels):
+            if not len(live):
+                break
+            if li and producer is not None:
+                for i in live.tolist():
+                    docs[i] = runtime._b(producer(i, results[i].authorization))
+                arena, offs, lens = pack(docs)
+            exprs = [e for c in level for e in (c.conditions, c.rules) if e is not None]
+            tri = err = sets = None
+            if exprs:
+                tri, err, sets = self._eval(exprs, live, arena, offs, lens)
+            col = {id(e): j for j, e in enumerate(exprs)}
+            denied = np.zeros(len(live), dtype=bool)
+            for c in level:
+                # evaluator-level `when` (auth_pipeline.go:120-125): not met -> ignored
+                ok_cond = np.ones(len(live), dtype=bool) if c.conditions is None else tri[col[id(c.conditions)]] == runtime.T
+                if c.rules is None:
+                    r_t = np.ones(len(live), dtype=bool)
+                    r_tri = None
+                else:
+                    r_tri = tri[col[id(c.rules)]]
+                    r_t = r_tri == runtime.T
+                for j in np.nonzero(ok_cond)[0]:
+                    i = live[j]
+                    if r_t[j]:
+                        results[i].authorization[c.name] = True  # json.go:26 -> setAuthorizationObj
+                    elif not denied[j]:
+                        denied[j] = True
+                        res = results[i]
+                        res.code = CODE_PERMISSION_DENIED
+                        res.denied_by = c.name
+                        if r_tri[j] == runtime.E:
+                            res.message = sets[col[id(c.rules)]].pattern_error(int(err[col[id(c.rules)]][j]))
+                        else:
+                            res.message = str(UnauthorizedError())
+            live = live[~denied]
+        return results
+
+
+def evaluate_json_authorization(rules: Optional[jsonexp.Expression], docs: Sequence):
+    """JSONPatternMatching.Call over a batch (authorization/json.go:15-27)."""
+    return JSONPatternMatching(rules).call_batch(docs)

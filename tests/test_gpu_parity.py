@@ -248,3 +248,32 @@ def test_line_engine_matches_oracle(ctx, workload, n):
         dec = ftri != 3
         assert np.array_equal(ftri[dec], gtri[dec])
         assert np.array_equal(fbm[dec], gbm[dec])
+
+
+def test_pipeline_batch_on_device():
+    """The batched `when` + authorization phase (authorino_amd.pipeline) on the device
+    against the same phase evaluated with the oracle (tests/test_pipeline_host.py)."""
+    from test_pipeline_host import OracleCtx, _doc
+
+    from authorino_amd import jsonexp as J
+    from authorino_amd import pipeline as P
+
+    rng = np.random.default_rng(8)
+    subs, groups = ["alice", "bob", "carol"], ["users", "admins", "devs"]
+    cfgs = []
+    for k in range(8):
+        rules = J.Any(J.Pattern("auth.identity.sub", J.EqualOperator, str(rng.choice(subs))),
+                      J.Pattern("auth.identity.groups", J.IncludesOperator, str(rng.choice(groups))))
+        cond = None if k % 3 == 0 else J.All(
+            J.Pattern("context.request.http.path", J.RegexOperator, "^/" + str(rng.choice(["api", "op", "a"]))))
+        cfgs.append(P.AuthorizationConfig(f"c{k}", rules=rules, conditions=cond, priority=k % 3))
+    cfgs.append(P.AuthorizationConfig("bad", rules=J.All(J.Pattern("x", J.RegexOperator, "(")), priority=3))
+    cfg = P.AuthConfig(conditions=J.All(J.Pattern("context.request.http.path", J.NotEqualOperator, "/x")),
+                       authorization=cfgs)
+    docs = [_doc(str(rng.choice(["/operation", "/api/v1", "/admin", "/x"])), str(rng.choice(subs)),
+                 list(rng.choice(groups, size=2, replace=False))) for _ in range(2000)]
+    got = P.AuthPipelineBatch(cfg).evaluate(docs)
+    want = P.AuthPipelineBatch(cfg, ctx=OracleCtx()).evaluate(docs)
+    for g, w in zip(got, want):
+        assert (g.code, g.message, g.skipped, g.denied_by, g.authorization) == \
+               (w.code, w.message, w.skipped, w.denied_by, w.authorization)
