@@ -538,14 +538,205 @@ AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t
     return scan_doc<MODE>(blob, blob_tables(blob), d, n, row, load);
 }
 
+// String() of a value when it needs no formatting: a byte span (unescaped string,
+// integer, raw JSON) or one of the literals true / false / "" (Null). Returned by value
+// (no out-pointers, no indexed arrays): the general path's StrSrc / RuneReader carry
+// small indexed buffers, which the compiler places in scratch memory.
+// the 4 bytes at p when only `avail` (>= 1) of them are readable: no aligned dword past
+// the one holding p[avail - 1] is touched (bytes past it are garbage)
+AJX_HD uint32_t load_u32_upto(const uint8_t* p, uint32_t avail) {
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t* q = (const uint32_t*)(p - sh);
+    const uint32_t w0 = q[0];
+    const uint32_t w1 = (sh && avail > 4u - sh) ? q[1] : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbyte(w1, w0, sh);
+#else
+    return sh ? (w0 >> (8 * sh)) | (w1 << (32 - 8 * sh)) : w0;
+#endif
+}
+
+struct RawVal {
+    uint32_t a, n;  // span in the document
+    uint32_t lit;   // 0 span, kLitTrue / kLitFalse / kLitEmpty for the literals
+    bool ok;        // false: the general path formats it
+};
+AJX_HD RawVal raw_value(const uint8_t* doc, const ValueRef& v) {
+    RawVal r{v.start, v.end - v.start, 0u, true};
+    switch (v.type) {
+        case T_STRING:
+            r.a = v.start + 1;
+            r.n = v.end - v.start - 2;
+            r.ok = !v.esc;
+            break;
+        case T_NUMBER: {
+            uint32_t k = v.start;
+            if (k < v.end && doc[k] == '-') k++;
+            for (; k < v.end; k += 4) {  // -?[0-9]* is its own String()
+                const uint32_t w = load_u32_upto(doc + k, v.end - k);
+                const uint32_t m = v.end - k >= 4 ? 0xFFFFFFFFu : (1u << (8 * (v.end - k))) - 1u;
+                const uint32_t d = w ^ 0x30303030u;
+                if ((((d + 0x76767676u) | d) & 0x80808080u) & m) { r.ok = false; break; }
+            }
+            break;
+        }
+        case T_TRUE: r.lit = kLitTrue; r.n = 4; break;
+        case T_FALSE: r.lit = kLitFalse; r.n = 5; break;
+        case T_JSON: break;
+        default: r.lit = kLitEmpty; r.n = 0; break;  // Null: ""
+    }
+    return r;
+}
+
+// `matches` on a raw span: ASCII four bytes at a time, utf8.DecodeRune otherwise (the
+// S_RAW branch of dfa_match without a StrSrc)
+AJX_HD bool dfa_match_span(const uint8_t* blob, uint32_t dfa_off, const uint8_t* p, uint32_t n) {
+    const DfaHdr* h = (const DfaHdr*)(blob + dfa_off);
+    const uint16_t* tr = (const uint16_t*)(blob + h->trans_off);
+    const uint32_t nc = h->n_classes, ms = h->match_state;
+    uint32_t st = h->start;
+    if (st == ms) return true;
+    uint32_t i = 0;
+    while (i < n) {
+        if (i + 4 <= n) {
+            const uint32_t w = load_u32_any(p + i);
+            if (!(w & 0x80808080u)) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    st = tr[st * nc + h->ascii_class[(w >> (8 * k)) & 0x7Fu]];
+                    if (st == ms) return true;
+                }
+                i += 4;
+                continue;
+            }
+        }
+        const uint32_t b0 = p[i];
+        int32_t r = (int32_t)b0;
+        uint32_t sz = 1;
+        if (b0 >= 0x80) {
+            r = 0xFFFD;
+            uint32_t need = 0, lo = 0x80, hi = 0xBF, v = 0;
+            if (b0 >= 0xC2 && b0 <= 0xDF) { need = 2; v = b0 & 0x1F; }
+            else if (b0 >= 0xE0 && b0 <= 0xEF) {
+                need = 3; v = b0 & 0x0F;
+                if (b0 == 0xE0) lo = 0xA0;
+                if (b0 == 0xED) hi = 0x9F;
+            } else if (b0 >= 0xF0 && b0 <= 0xF4) {
+                need = 4; v = b0 & 0x07;
+                if (b0 == 0xF0) lo = 0x90;
+                if (b0 == 0xF4) hi = 0x8F;
+            }
+            if (need && n - i >= need && p[i + 1] >= lo && p[i + 1] <= hi) {
+                bool good = true;
+                v = (v << 6) | (p[i + 1] & 0x3Fu);
+                for (uint32_t k = 2; k < need; k++) {
+                    const uint32_t c = p[i + k];
+                    if (c < 0x80 || c > 0xBF) { good = false; break; }
+                    v = (v << 6) | (c & 0x3Fu);
+                }
+                if (good) { r = (int32_t)v; sz = need; }
+            }
+        }
+        i += sz;
+        st = tr[st * nc + rune_class(h, blob, r)];
+        if (st == ms) return true;
+    }
+    return blob[h->eot_off + st] != 0;
+}
+// `matches` on a literal's text ("true" / "false" / ""), from registers
+AJX_HD bool dfa_match_lit(const uint8_t* blob, uint32_t dfa_off, uint32_t lit) {
+    const DfaHdr* h = (const DfaHdr*)(blob + dfa_off);
+    const uint16_t* tr = (const uint16_t*)(blob + h->trans_off);
+    const uint32_t nc = h->n_classes, ms = h->match_state;
+    uint32_t st = h->start;
+    if (st == ms) return true;
+    const uint64_t text = lit == kLitTrue ? 0x65757274ull : lit == kLitFalse ? 0x65736C6166ull : 0ull;
+    const uint32_t n = lit == kLitTrue ? 4u : lit == kLitFalse ? 5u : 0u;
+    for (uint32_t k = 0; k < n; k++) {
+        st = tr[st * nc + h->ascii_class[(text >> (8 * k)) & 0x7Fu]];
+        if (st == ms) return true;
+    }
+    return blob[h->eot_off + st] != 0;
+}
+
+// eq on a raw value
+AJX_HD bool raw_equals(const uint8_t* doc, const RawVal& r, const Pattern& pt, const uint8_t* lits) {
+    if (r.lit) return (pt.litf & r.lit) != 0;
+    return r.n == pt.lit_len && bytes_equal(doc + r.a, lits + pt.lit_off, r.n);
+}
+
+// incl / excl of every such pattern of one selector, the array walked once: bit j of the
+// result = pattern j of the selector's list found among the elements. Compact arrays of
+// unescaped strings / integers / literals only; false sends the selector to the general
+// path (whitespace, escapes, nested containers, non-integer numbers, a non-array value).
+AJX_HD bool incl_hits(const uint8_t* doc, const ValueRef& v, const Pattern* pats, const uint16_t* plist,
+                      uint32_t begin, uint32_t cnt, const uint8_t* lits, uint32_t* hits) {
+    uint32_t h = 0;
+    if (v.type != T_JSON || v.end - v.start < 2 || doc[v.start] != '[') return false;
+    uint32_t i = v.start + 1;
+    const uint32_t end = v.end - 1;  // the ']'
+    if (doc[end] != ']') return false;
+    while (i < end) {
+        ValueRef e;
+        const uint32_t c = doc[i];
+        e.start = i;
+        e.esc = 0;
+        if (c == '"') {  // the closing quote: the first '"' or '\\' after i
+            uint32_t k = i + 1;
+            for (;;) {
+                if (k >= end) return false;
+                const uint32_t w = load_u32_upto(doc + k, end + 1 - k);
+                const uint32_t m = end - k >= 4 ? 0xFFFFFFFFu : (1u << (8 * (end - k))) - 1u;
+                const uint32_t f = (eq_bytes(w, 0x22222222u) | eq_bytes(w, 0x5C5C5C5Cu)) & m;
+                if (f) {
+                    k += (uint32_t)__builtin_ctz(f) >> 3;
+                    break;
+                }
+                k += 4;
+            }
+            if (doc[k] != '"') return false;  // an escape
+            e.end = k + 1;
+            e.type = T_STRING;
+        } else if (c == 't' || c == 'f' || c == 'n') {
+            const uint32_t w = load_u32_upto(doc + i, end + 1 - i);
+            if (w == 0x65757274u) { e.end = i + 4; e.type = T_TRUE; }
+            else if (w == 0x6C6C756Eu) { e.end = i + 4; e.type = T_NULL; }
+            else if (w == 0x736C6166u && i + 4 < end && doc[i + 4] == 'e') { e.end = i + 5; e.type = T_FALSE; }
+            else return false;
+        } else if (c == '-' || (c >= '0' && c <= '9')) {
+            uint32_t k = i + 1;
+            while (k < end && doc[k] != ',') k++;
+            e.end = k;
+            e.type = T_NUMBER;
+        } else {
+            return false;
+        }
+        const RawVal r = raw_value(doc, e);
+        if (!r.ok) return false;
+        for (uint32_t j = 0; j < cnt; j++) {
+            const Pattern pt = pats[plist[begin + j]];
+            if ((pt.op == OP_INCL || pt.op == OP_EXCL) && pt.state == P_OK && raw_equals(doc, r, pt, lits))
+                h |= 1u << j;
+        }
+        i = e.end;
+        if (i < end) {
+            if (doc[i] != ',') return false;
+            i++;
+            if (i == end) return false;  // "[1,]"
+        }
+    }
+    *hits = h;
+    return true;
+}
+
 // Stage B for one request: patterns on the captured values, bitmap, fold.
 // res(p) values are V_T / V_F / V_E / V_U.
 AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, const uint64_t* row, uint64_t t[2],
                               uint64_t u[2]) {
     // selector by selector: each captured value is decoded once for all its patterns;
-    // when its String() is a contiguous byte span (unescaped string, integer, literal,
-    // raw JSON) eq/neq compare a dword at a time and `matches` runs the DFA straight
-    // over the span
+    // when its String() is a byte span or a literal, eq/neq compare a dword at a time,
+    // `matches` runs the DFA straight over the span and incl/excl walk a compact array
+    // once for all of the selector's patterns; other values take eval_pattern
     const RulesetHdr* h = (const RulesetHdr*)blob;
     const Pattern* pats = (const Pattern*)(blob + h->off_patterns);
     const SelectorPatterns* sps = (const SelectorPatterns*)(blob + h->off_sel_patterns);
@@ -570,22 +761,24 @@ AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, const uin
         v.end = v.start + (meta & 0xFFFFFFu);
         v.type = (uint8_t)((meta >> 24) & 7u);
         v.esc = (uint8_t)((meta >> 27) & 1u);
-        StrSrc base;
-        const bool raw = string_of(doc, v, &base) && base.kind == StrSrc::S_RAW;
-        const uint8_t* rp = raw ? base.p + base.i : doc;
-        const uint32_t rn = raw ? base.n - base.i : 0u;
+        const RawVal rv = raw_value(doc, v);
         const uint32_t begin = sps[s].begin;
+        uint32_t hits = 0;
+        const bool fast_incl = cnt <= 32 && incl_hits(doc, v, pats, plist, begin, cnt, lits, &hits);
         for (uint32_t j = 0; j < cnt; j++) {
             const uint32_t p = plist[begin + j];
             const Pattern pt = pats[p];
             uint8_t r;
-            if (raw && (pt.op == OP_EQ || pt.op == OP_NEQ)) {
-                const bool eq = rn == pt.lit_len && bytes_equal(rp, lits + pt.lit_off, rn);
-                r = eq == (pt.op == OP_EQ) ? V_T : V_F;
-            } else if (raw && pt.op == OP_MATCHES) {
-                StrSrc sc;
-                sc.init_raw(rp, 0, rn);
-                r = dfa_match(blob, pt.dfa_off, &sc) ? V_T : V_F;
+            if (pt.state != P_OK) {
+                r = pt.state == P_STATIC_E ? V_E : V_U;
+            } else if (rv.ok && (pt.op == OP_EQ || pt.op == OP_NEQ)) {
+                r = raw_equals(doc, rv, pt, lits) == (pt.op == OP_EQ) ? V_T : V_F;
+            } else if (rv.ok && pt.op == OP_MATCHES) {
+                const bool m = rv.lit ? dfa_match_lit(blob, pt.dfa_off, rv.lit)
+                                      : dfa_match_span(blob, pt.dfa_off, doc + rv.a, rv.n);
+                r = m ? V_T : V_F;
+            } else if (fast_incl && (pt.op == OP_INCL || pt.op == OP_EXCL)) {
+                r = (((hits >> j) & 1u) != 0) == (pt.op == OP_INCL) ? V_T : V_F;
             } else {
                 r = eval_pattern(blob, pt, doc, v);
             }

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void ajx_patterns(const uint8_t* const* __rest
 // request's value bytes are still in cache (a separate stage-B launch re-reads them
 // from HBM). Requests stage A can not prove gjson-equivalent go to the slow list.
 template <bool SHARED>
-__global__ __launch_bounds__(256) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
+__global__ __launch_bounds__(256, 4) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
                                                       const uint32_t* __restrict__ set_of_req,
                                                       const uint8_t* __restrict__ arena,
                                                       const uint64_t* __restrict__ offs,

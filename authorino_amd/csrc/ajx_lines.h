@@ -847,12 +847,15 @@ struct LineScan {
             const uint32_t o_elem = open_ok & tcap_here & arr;  // an element container of the innermost capture opens
             const uint32_t npush = vd_leaf + v_elem + cap_close + c_elem;
             // rare tokens take the general path
-            const uint32_t rare =
+            uint32_t rare =
                 ok & (((npush - 1u) >> 31 ^ 1u) & (npush != 1u ? 1u : 0u)  // two values at once
                       | (f_gap & (sc_ok ^ 1u))                                // a long / odd scalar
                       | (f_gap & ((vd_leaf | v_elem) & (sc_raw ^ 1u)))        // a number String() reformats
                       | (idx_arr & live_here) | (close_ok & (idx_bits >> (depth - 1u)) & 1u)
                       | (o_cap & (ncap >> 1)));                               // a third nested capture
+#ifdef AJX_LINES_BRANCHY
+            rare = ok;  // profiling: every token through the general (branchy) path
+#endif
 #ifdef AJX_COUNT_RARE
             if (rare) {
                 extern uint64_t ajx_rare_counts[8];
