@@ -56,10 +56,49 @@ struct Block16 {
     uint32_t x, y, z, w;
 };
 
+AJX_HD uint32_t ctz64f(uint64_t x) { return (uint32_t)__builtin_ctzll(x); }
+AJX_HD uint32_t hibit64f(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
+AJX_HD uint32_t popc64f(uint64_t x) { return (uint32_t)__builtin_popcountll(x); }
+AJX_HD uint64_t below64f(uint32_t i) { return i >= 64 ? ~0ull : ((1ull << i) - 1ull); }
+
+// The document window ring of one work-item: the current and the previous 64-byte
+// window. Chunk j (16 B) of the ring — j = (A >> 4) & 7 for the position A relative to
+// the document's first aligned 16-B block — sits at j * cstride + lane16, so a wave's
+// 16-B accesses to one chunk index are contiguous (conflict-free ds_write_b128).
+struct WinRing {
+    uint8_t* base;
+    uint32_t lane16;   // lane * 16
+    uint32_t cstride;  // lanes * 16
+    AJX_HD uint32_t off(uint32_t a) const { return ((a >> 4) & 7u) * cstride + lane16 + (a & 15u); }
+    AJX_HD uint32_t u8(uint32_t a) const { return base[off(a)]; }
+    AJX_HD uint32_t u32a(uint32_t a) const { return *reinterpret_cast<const uint32_t*>(base + off(a)); }  // a % 4 == 0
+    AJX_HD uint64_t u64(uint32_t a) const {  // the 8 bytes at a, little-endian
+        const uint32_t q = a & ~3u, sh = a & 3u;
+        const uint32_t w0 = u32a(q), w1 = u32a(q + 4), w2 = u32a(q + 8);
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+#else
+        const uint32_t lo = sh ? (w0 >> (8 * sh)) | (w1 << (32 - 8 * sh)) : w0;
+        const uint32_t hi = sh ? (w1 >> (8 * sh)) | (w2 << (32 - 8 * sh)) : w1;
+#endif
+        return (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    AJX_HD void put(uint32_t a, const Block16& b) {  // a % 16 == 0
+#if defined(__HIP_DEVICE_COMPILE__)
+        *reinterpret_cast<uint4*>(base + off(a)) = uint4{b.x, b.y, b.z, b.w};
+#else
+        *reinterpret_cast<Block16*>(base + off(a)) = b;
+#endif
+    }
+};
+
 // Stage-A scanner state (kept in registers; no dynamically indexed arrays). The trie
 // tables are read through `tn`/`tc`, which the kernel points at an LDS copy when the
-// whole batch uses one ruleset; document bytes a token needs (key tails, literals) come
-// from the previous/current block registers, global memory only on rare paths.
+// whole batch uses one ruleset; document bytes a token needs (its byte, a key's last
+// 8 bytes, a short scalar) come from the window ring, global memory only on rare paths.
+// The document goes by in 64-byte windows: one classification per window and one token
+// loop over its 64-bit token mask (a wave runs each loop as long as its busiest lane,
+// so wider windows even out the lanes' token counts).
 struct Scan {
     const TrieNode* tn;
     const TrieChild* tc;
@@ -69,14 +108,14 @@ struct Scan {
     const uint8_t* d;
     uint64_t* row;  // capture row (header + records)
     uint32_t n;
+    WinRing ring;
 
-    uint64_t ph;        // bytes 8..15 of the previous 16-byte block
-    uint64_t cl, chh;   // bytes 0..7 / 8..15 of the current block
-    int32_t bpos;       // doc position of the current block's byte 0
-    uint32_t mbs;       // backslash bits of the current block
-    uint32_t carry_bs;  // last backslash before the current block (~0u none)
-    uint32_t oq;        // opening-quote bits of the current block
-    uint32_t carry_oq;  // last opening quote before the current block
+    uint32_t wa;        // ring position of the current window's byte 0
+    int32_t bpos;       // doc position of the current window's byte 0
+    uint64_t mbs;       // backslash bits of the current window
+    uint32_t carry_bs;  // last backslash before the current window (~0u none)
+    uint64_t oq;        // opening-quote bits of the current window
+    uint32_t carry_oq;  // last opening quote before the current window
     uint32_t last_oq;
 
     uint64_t is_arr;    // bit k: container at depth k (1-based) is an array
@@ -94,28 +133,21 @@ struct Scan {
 
     // (values are selected after they are computed, never by member address: that keeps
     // the scanner state in registers)
-    AJX_HD static uint64_t funnel64(uint64_t a, uint64_t b, uint32_t sh) {  // ({b,a} >> sh) low 64, sh < 64
-        return sh ? (a >> sh) | (b << (64 - sh)) : a;
-    }
-    // the 8 document bytes ending just before current-block offset q (0..16), little-endian
+    // the 8 document bytes ending just before window offset q (0..64), little-endian
     AJX_HD uint64_t tail8(uint32_t q) const {
-        const uint64_t r1 = funnel64(ph, cl, (q & 7u) * 8);
-        const uint64_t r2 = funnel64(cl, chh, (q & 7u) * 8);
-        const uint64_t r3 = chh;
-        return q < 8 ? r1 : (q < 16 ? r2 : r3);
+        const int32_t a = (int32_t)(wa + q) - 8;
+        if (a < 0) return ring.u64(0) << (8 * (uint32_t)(-a));  // (before the first block: zeros)
+        return ring.u64((uint32_t)a);
     }
-    AJX_HD uint32_t byte_at(uint32_t i) const {
-        const uint64_t v0 = cl >> ((i & 7u) * 8), v1 = chh >> ((i & 7u) * 8);
-        return (uint32_t)(i < 8 ? v0 : v1) & 0xFFu;
-    }
-    // opening quote of the string whose closing quote is at current-block offset i
+    AJX_HD uint32_t byte_at(uint32_t i) const { return ring.u8(wa + i); }
+    // opening quote of the string whose closing quote is at window offset i
     AJX_HD uint32_t open_before(uint32_t i) const {
-        const uint32_t ob = oq & ((1u << i) - 1u);
-        return ob ? (uint32_t)(bpos + (int32_t)hibit32(ob)) : carry_oq;
+        const uint64_t ob = oq & below64f(i);
+        return ob ? (uint32_t)(bpos + (int32_t)hibit64f(ob)) : carry_oq;
     }
     AJX_HD uint32_t last_bs_before(uint32_t i) const {
-        const uint32_t mb = mbs & ((1u << i) - 1u);
-        return mb ? (uint32_t)(bpos + (int32_t)hibit32(mb)) : carry_bs;
+        const uint64_t mb = mbs & below64f(i);
+        return mb ? (uint32_t)(bpos + (int32_t)hibit64f(mb)) : carry_bs;
     }
 
     AJX_HD uint32_t node_at(uint32_t dd) const {
@@ -346,100 +378,110 @@ struct Scan {
         }
     }
 
-    // process the 16 document bytes of aligned block `blk` (doc position of byte 0 = bp)
+    // process the 64 document bytes of window `blk` (ring position of byte 0 = a, a
+    // multiple of 64; doc position of byte 0 = bp)
     template <int MODE = 0>
-    AJX_HD void block(const Block16& blk, int32_t bp) {
-        ph = chh;
-        cl = (uint64_t)blk.x | ((uint64_t)blk.y << 32);
-        chh = (uint64_t)blk.z | ((uint64_t)blk.w << 32);
+    AJX_HD void window(const Block16* blk, uint32_t a, int32_t bp) {
+        wa = a;
         bpos = bp;
-        uint32_t valid = 0xFFFFu;
-        if (bp < 0) valid &= 0xFFFFu << (uint32_t)(-bp);
-        if (bp + 16 > (int32_t)n) valid &= 0xFFFFu >> (uint32_t)(bp + 16 - (int32_t)n);
-        uint32_t mq = 0, mst = 0, mws = 0;
-        mbs = 0;
+        uint64_t valid = ~0ull;
+        if (bp < 0) valid &= ~below64f((uint32_t)(-bp));
+        if (bp + 64 > (int32_t)n) valid &= below64f((uint32_t)((int32_t)n - bp));
+        uint64_t mq = 0, mst = 0, mws = 0, mb = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t x = k == 0 ? blk.x : k == 1 ? blk.y : k == 2 ? blk.z : blk.w;
-            const uint32_t lx = x | 0x20202020u;
-            mq |= gather4(eq_bytes(x, 0x22222222u)) << (4 * k);
-            mbs |= gather4(eq_bytes(x, 0x5C5C5C5Cu)) << (4 * k);
-            mst |= gather4(eq_bytes(lx, 0x7B7B7B7Bu) | eq_bytes(lx, 0x7D7D7D7Du) | eq_bytes(x, 0x3A3A3A3Au) |
-                           eq_bytes(x, 0x2C2C2C2Cu))
-                   << (4 * k);
-            mws |= gather4(le20_bytes(x)) << (4 * k);
+        for (int j = 0; j < 4; j++) {
+            const Block16 x4 = blk[j];
+            ring.put(a + 16u * (uint32_t)j, x4);
+            uint32_t q16 = 0, b16 = 0, s16 = 0, w16 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t x = k == 0 ? x4.x : k == 1 ? x4.y : k == 2 ? x4.z : x4.w;
+                const uint32_t lx = x | 0x20202020u;
+                q16 |= gather4(eq_bytes(x, 0x22222222u)) << (4 * k);
+                b16 |= gather4(eq_bytes(x, 0x5C5C5C5Cu)) << (4 * k);
+                s16 |= gather4(eq_bytes(lx, 0x7B7B7B7Bu) | eq_bytes(lx, 0x7D7D7D7Du) | eq_bytes(x, 0x3A3A3A3Au) |
+                               eq_bytes(x, 0x2C2C2C2Cu))
+                       << (4 * k);
+                w16 |= gather4(le20_bytes(x)) << (4 * k);
+            }
+            mq |= (uint64_t)q16 << (16 * j);
+            mb |= (uint64_t)b16 << (16 * j);
+            mst |= (uint64_t)s16 << (16 * j);
+            mws |= (uint64_t)w16 << (16 * j);
         }
         mq &= valid;
-        mbs &= valid;
+        mb &= valid;
         mst &= valid;
         mws &= valid;
+        mbs = mb;
         // escaped bytes: the byte after an odd-length backslash run
-        uint32_t escaped;
+        uint64_t escaped;
         {
-            const uint32_t bs = mbs & ~esc;
-            const uint32_t follows = ((bs << 1) | esc) & 0xFFFFu;
-            const uint32_t even = 0x5555u;
-            const uint32_t odd_starts = bs & ~even & ~follows;
-            const uint32_t seq = odd_starts + bs;
-            esc = (seq >> 16) & 1u;
-            escaped = (even ^ ((seq << 1) & 0xFFFFu)) & follows;
+            const uint64_t bs = mb & ~(uint64_t)esc;
+            const uint64_t follows = (bs << 1) | esc;
+            const uint64_t even = 0x5555555555555555ull;
+            const uint64_t odd_starts = bs & ~even & ~follows;
+            const uint64_t seq = odd_starts + bs;
+            esc = seq < bs ? 1u : 0u;  // carry out of the window
+            escaped = (even ^ (seq << 1)) & follows;
         }
         carry_bs = last_bs;
-        if (mbs) last_bs = (uint32_t)(bp + (int32_t)hibit32(mbs));
-        const uint32_t qu = mq & ~escaped;
-        uint32_t x = qu;
+        if (mb) last_bs = (uint32_t)(bp + (int32_t)hibit64f(mb));
+        const uint64_t qu = mq & ~escaped;
+        uint64_t x = qu;
         x ^= x << 1;
         x ^= x << 2;
         x ^= x << 4;
         x ^= x << 8;
-        x &= 0xFFFFu;
-        const uint32_t instr = in_str ? (x ^ 0xFFFFu) : x;  // inside a string after this byte
-        in_str = (instr >> 15) & 1u;
-        const uint32_t outside = ~instr & ~qu & valid;
-        if (mbs & outside) { st = X_SLOW; return; }  // backslash outside any string
-        const uint32_t ns = outside & ~mst & ~mws;    // scalar bytes
+        x ^= x << 16;
+        x ^= x << 32;
+        const uint64_t instr = in_str ? ~x : x;  // inside a string after this byte
+        in_str = (uint32_t)(instr >> 63);
+        const uint64_t outside = ~instr & ~qu & valid;
+        if (mb & outside) { st = X_SLOW; return; }  // backslash outside any string
+        const uint64_t ns = outside & ~mst & ~mws;    // scalar bytes
         // tokens: structural bytes outside strings and closing quotes (an opening quote
         // is the quote after which the string is open)
         oq = qu & instr;
         carry_oq = last_oq;
-        if (oq) last_oq = (uint32_t)(bp + (int32_t)hibit32(oq));
-        uint32_t toks = ((mst & outside) | (qu & ~instr)) & 0xFFFFu;
+        if (oq) last_oq = (uint32_t)(bp + (int32_t)hibit64f(oq));
+        uint64_t toks = (mst & outside) | (qu & ~instr);
         if constexpr (MODE == 2) {  // ablation: classification only
-            gap_cnt += popc32(toks) + popc32(ns);
+            gap_cnt += popc64f(toks) + popc64f(ns);
             return;
         }
-        uint32_t below = 0;  // bits already consumed
+        uint64_t below = 0;  // bits already consumed
         while (toks) {
-            const uint32_t i = ctz32(toks);
+            const uint32_t i = ctz64f(toks);
             toks &= toks - 1;
-            const uint32_t g = ns & ((1u << i) - 1u) & ~below;
+            const uint64_t g = ns & below64f(i) & ~below;
             if (g) {
-                if (gap_cnt == 0) gap_first = (uint32_t)(bp + (int32_t)ctz32(g));
-                gap_last = (uint32_t)(bp + (int32_t)hibit32(g));
-                gap_cnt += popc32(g);
+                if (gap_cnt == 0) gap_first = (uint32_t)(bp + (int32_t)ctz64f(g));
+                gap_last = (uint32_t)(bp + (int32_t)hibit64f(g));
+                gap_cnt += popc64f(g);
             }
-            below = (2u << i) - 1u;
+            below = below64f(i + 1);
             token(byte_at(i), i);
             if (st >= X_DONE) return;
             // compact JSON: the ':' right after a key and the ',' right after a value are
             // taken in the same iteration
             const uint32_t nb = i + 1;
-            if ((toks >> nb) & 1u) {
+            if (nb < 64 && ((toks >> nb) & 1u)) {
                 const uint32_t c2 = byte_at(nb);
                 const bool colon = st == X_COLON && c2 == ':';
                 const bool comma = st == X_COMMA_OR_CLOSE && c2 == ',';
                 if (colon || comma) {
                     st = (colon || top_is_arr()) ? X_VALUE : X_KEY;
-                    toks &= ~(1u << nb);
-                    below = (2u << nb) - 1u;
+                    toks &= toks - 1;
+                    below = below64f(nb + 1);
                 }
             }
         }
-        const uint32_t g = ns & ~below & 0xFFFFu;
+        const uint64_t g = ns & ~below;
         if (g) {
-            if (gap_cnt == 0) gap_first = (uint32_t)(bp + (int32_t)ctz32(g));
-            gap_last = (uint32_t)(bp + (int32_t)hibit32(g));
-            gap_cnt += popc32(g);
+            if (gap_cnt == 0) gap_first = (uint32_t)(bp + (int32_t)ctz64f(g));
+            gap_last = (uint32_t)(bp + (int32_t)hibit64f(g));
+            gap_cnt += popc64f(g);
             if (st == X_ROOT) st = X_SLOW;  // a scalar (or junk) before the root container
         }
     }
@@ -457,12 +499,13 @@ AJX_HD Tables blob_tables(const uint8_t* blob) {
                   (const KeySlot*)(blob + h->off_key_slots)};
 }
 
-// Stage A for one request. `row` = capture row (1 + n_selectors u64). Returns true
-// when the row is valid (false: the request needs the exact scan).
+// Stage A for one request. `row` = capture row (1 + n_selectors u64); `ring` = the
+// work-item's window ring (128 B). Returns true when the row is valid (false: the
+// request needs the exact scan).
 // MODE (profiling ablations only): 0 = full scan, 1 = loads only, 2 = loads + classification
 template <int MODE = 0, class LoadBlock>
 AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, uint32_t n, uint64_t* row,
-                     LoadBlock load) {
+                     const WinRing& ring, LoadBlock load) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
     Scan s;
     s.tn = tab.tn;
@@ -473,7 +516,8 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     s.d = d;
     s.row = row;
     s.n = n;
-    s.ph = s.cl = s.chh = 0;
+    s.ring = ring;
+    s.wa = 0;
     s.bpos = 0;
     s.mbs = 0;
     s.carry_bs = ~0u;
@@ -500,19 +544,10 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
 #pragma unroll
     for (int j = 0; j < 4; j++) nxt[j] = load((uint32_t)(4 + j), nblk);
     for (uint32_t b0 = 0; b0 < nblk; b0 += 4) {
-        // one copy of the block body (the window shifts down instead of unrolling j:
-        // the token machine is large and four inlined copies thrash the I-cache)
-#pragma unroll 1
-        for (uint32_t j = 0; j < 4; j++) {
-            const uint32_t b = b0 + j;
-            if constexpr (MODE == 1) {
-                if (b < nblk) s.found ^= (uint64_t)(cur[0].x ^ cur[0].y ^ cur[0].z ^ cur[0].w) << j;
-            } else {
-                if (b < nblk && s.st < X_DONE) s.block<MODE>(cur[0], (int32_t)(b * 16) - (int32_t)mis);
-            }
-            cur[0] = cur[1];
-            cur[1] = cur[2];
-            cur[2] = cur[3];
+        if constexpr (MODE == 1) {
+            s.found ^= (uint64_t)(cur[0].x ^ cur[1].y ^ cur[2].z ^ cur[3].w) << (b0 & 31);
+        } else {
+            s.window<MODE>(cur, b0 * 16, (int32_t)(b0 * 16) - (int32_t)mis);
         }
         if (s.st >= X_DONE) break;
 #pragma unroll
@@ -533,15 +568,6 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     return true;
 }
 
-template <int MODE = 0, class LoadBlock>
-AJX_HD bool scan_doc(const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t* row, LoadBlock load) {
-    return scan_doc<MODE>(blob, blob_tables(blob), d, n, row, load);
-}
-
-// String() of a value when it needs no formatting: a byte span (unescaped string,
-// integer, raw JSON) or one of the literals true / false / "" (Null). Returned by value
-// (no out-pointers, no indexed arrays): the general path's StrSrc / RuneReader carry
-// small indexed buffers, which the compiler places in scratch memory.
 // the 4 bytes at p when only `avail` (>= 1) of them are readable: no aligned dword past
 // the one holding p[avail - 1] is touched (bytes past it are garbage)
 AJX_HD uint32_t load_u32_upto(const uint8_t* p, uint32_t avail) {

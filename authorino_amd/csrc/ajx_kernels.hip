@@ -131,16 +131,32 @@ __device__ __forceinline__ const uint8_t* stage_blob(const uint8_t* gblob) {
     }
 }
 
+// the work-item's 128-B window ring in dynamic LDS: [blob copy (SHARED)] [ring: per wave
+// 8 chunks x 64 lanes x 16 B]
+constexpr uint32_t kWinRingBytesPerWave = 8 * 64 * 16;
+// single-pass workgroups of up to 8 waves: one LDS copy of the ruleset blob per 8 waves,
+// so blob + rings of 16 waves fit a CU's 160 KiB for blobs up to ~16 KiB (4 waves/SIMD)
+constexpr uint32_t kFastBlock = 512;
+__device__ __forceinline__ WinRing lane_ring(uint32_t ring_off) {
+    extern __shared__ uint4 s_dyn_ring[];
+    WinRing r;
+    r.base = reinterpret_cast<uint8_t*>(s_dyn_ring) + ring_off + (threadIdx.x >> 6) * kWinRingBytesPerWave;
+    r.lane16 = (threadIdx.x & 63u) * 16u;
+    r.cstride = 64u * 16u;
+    return r;
+}
+
 // stage A for request r: single-pass scan into its capture row (false: slow list)
 template <int MODE>
-__device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t* d, uint32_t len, uint64_t* row) {
+__device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t* d, uint32_t len, uint64_t* row,
+                                             const WinRing& ring) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     if (!(h->flags & kFlagFastOk) || len >= (1u << 24)) {
         row[0] = kRowSlow;
         return false;
     }
     const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-    return scan_doc<MODE>(blob, blob_tables(blob), d, len, row, [&](uint32_t b, uint32_t nblk) -> Block16 {
+    return scan_doc<MODE>(blob, blob_tables(blob), d, len, row, ring, [&](uint32_t b, uint32_t nblk) -> Block16 {
         if (b < nblk) {
             const uint4 v = a4[b];
             return Block16{v.x, v.y, v.z, v.w};
@@ -173,24 +189,24 @@ __device__ __forceinline__ void finish_request(uint32_t r, const uint8_t* blob, 
 // Stage A alone (profiling split / ablations): structural scan -> capture rows.
 // MODE 1/2 are the loads-only / loads+classification ablations.
 template <int MODE, bool SHARED>
-__global__ __launch_bounds__(256) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
+__global__ __launch_bounds__(kFastBlock, 4) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
                                                      const uint32_t* __restrict__ set_of_req,
                                                      const uint8_t* __restrict__ arena,
                                                      const uint64_t* __restrict__ offs,
                                                      const uint32_t* __restrict__ lens, uint32_t n,
                                                      uint64_t* __restrict__ rows, uint32_t row_stride,
                                                      uint32_t* __restrict__ slow_count,
-                                                     uint32_t* __restrict__ slow_ids) {
+                                                     uint32_t* __restrict__ slow_ids, uint32_t ring_off) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)]);
     if (r >= n) return;
-    if (!scan_request<MODE>(blob, arena + offs[r], lens[r], rows + (size_t)r * row_stride))
+    if (!scan_request<MODE>(blob, arena + offs[r], lens[r], rows + (size_t)r * row_stride, lane_ring(ring_off)))
         slow_ids[atomicAdd(slow_count, 1u)] = r;
 }
 
 // Stage B alone (profiling split): patterns on the captured values, bitmap, fold
 template <bool SHARED>
-__global__ __launch_bounds__(256) void ajx_patterns(const uint8_t* const* __restrict__ sets,
+__global__ __launch_bounds__(kFastBlock) void ajx_patterns(const uint8_t* const* __restrict__ sets,
                                                     const uint32_t* __restrict__ set_of_req,
                                                     const uint8_t* __restrict__ arena,
                                                     const uint64_t* __restrict__ offs, uint32_t n,
@@ -209,7 +225,7 @@ __global__ __launch_bounds__(256) void ajx_patterns(const uint8_t* const* __rest
 // request's value bytes are still in cache (a separate stage-B launch re-reads them
 // from HBM). Requests stage A can not prove gjson-equivalent go to the slow list.
 template <bool SHARED>
-__global__ __launch_bounds__(256, 4) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
+__global__ __launch_bounds__(kFastBlock, 4) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
                                                       const uint32_t* __restrict__ set_of_req,
                                                       const uint8_t* __restrict__ arena,
                                                       const uint64_t* __restrict__ offs,
@@ -218,13 +234,13 @@ __global__ __launch_bounds__(256, 4) void ajx_scan_fused(const uint8_t* const* _
                                                       uint32_t* __restrict__ slow_count,
                                                       uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
                                                       int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
-                                                      uint32_t stride) {
+                                                      uint32_t stride, uint32_t ring_off) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)]);
     if (r >= n) return;
     uint64_t* row = rows + (size_t)r * row_stride;
     const uint8_t* d = arena + offs[r];
-    if (!scan_request<0>(blob, d, lens[r], row)) {
+    if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off))) {
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
@@ -354,26 +370,42 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
                             int mode) {
     if (n == 0) return hipSuccess;
-    const uint32_t block = 256;
-    const uint32_t grid = (n + block - 1) / block;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
-    const uint32_t lds = shared ? shared_blob_bytes : 0u;
+    // small blobs: 4-wave groups (measured faster on c2); larger ones share one copy per
+    // 8 waves (c3)
+    const uint32_t block = shared && shared_blob_bytes <= 8192 ? 256u : kFastBlock;
+    const uint32_t grid = (n + block - 1) / block;
+    // dynamic LDS of the single-pass kernels: [blob copy (shared)] [window rings]
+    const uint32_t ring_off = shared ? (shared_blob_bytes + 15u) & ~15u : 0u;
+    const uint32_t lds = ring_off + (block / 64) * kWinRingBytesPerWave;
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
+    static bool fast_attr_set = false;
+    if (!fast_attr_set) {
+        const void* ks[] = {reinterpret_cast<const void*>(&ajx_scan_fast<0, true>),
+                            reinterpret_cast<const void*>(&ajx_scan_fast<0, false>),
+                            reinterpret_cast<const void*>(&ajx_scan_fast<1, true>),
+                            reinterpret_cast<const void*>(&ajx_scan_fast<2, true>),
+                            reinterpret_cast<const void*>(&ajx_scan_fused<true>),
+                            reinterpret_cast<const void*>(&ajx_scan_fused<false>)};
+        for (const void* k : ks)
+            if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
+                return e;
+        fast_attr_set = true;
+    }
     if (mode == 1 || mode == 2) {  // profiling ablations of stage A (uniform ruleset only)
         if (!shared) return hipErrorInvalidValue;
         if (mode == 1)
             hipLaunchKernelGGL((ajx_scan_fast<1, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off);
         else
             hipLaunchKernelGGL((ajx_scan_fast<2, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off);
         return hipGetLastError();
     }
     if (mode == 5 || mode >= 10) {  // the line engine; 11/12/13 profiling ablations
         const int lines_ablate = mode >= 10 ? mode - 10 : 0;
         const uint32_t lgrid = (n + kLinesBlock - 1) / kLinesBlock;
-        const uint32_t ring_off = shared ? (shared_blob_bytes + 15u) & ~15u : 0u;
         const uint32_t dyn = ring_off + (kLinesBlock / 64) * kRingBytesPerWave;
         static bool attr_set[2] = {false, false};
         if (!attr_set[shared]) {
@@ -397,13 +429,13 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     } else if (mode == 3) {  // profiling split: stage A and stage B as two launches
         if (shared) {
             hipLaunchKernelGGL((ajx_scan_fast<0, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            hipLaunchKernelGGL((ajx_patterns<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+            hipLaunchKernelGGL((ajx_patterns<true>), dim3(grid), dim3(block), ring_off, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
         } else {
-            hipLaunchKernelGGL((ajx_scan_fast<0, false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids);
+            hipLaunchKernelGGL((ajx_scan_fast<0, false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             hipLaunchKernelGGL((ajx_patterns<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
@@ -411,15 +443,15 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     } else if (shared) {  // mode 0 (default): the single-pass kernel
         hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
                            d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                           stride);
+                           stride, ring_off);
     } else {
-        hipLaunchKernelGGL((ajx_scan_fused<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
+        hipLaunchKernelGGL((ajx_scan_fused<false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
                            d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                           stride);
+                           stride, ring_off);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t sgrid = grid < 2048 ? grid : 2048;
-    hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
+    const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
+    hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(256), 0, stream, d_sets, d_set_of_req, d_arena,
                        d_offs, d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
     return hipGetLastError();
 }

@@ -138,7 +138,10 @@ int ht_eval_fast(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_
     std::memcpy(d, doc, len);
     std::vector<uint64_t> row(1 + hd->n_selectors, 0xDEADBEEFDEADBEEFull);
     const uint32_t* a = (const uint32_t*)(d - mis);
-    bool ok = scan_doc(blob, d, len, row.data(), [&](uint32_t b, uint32_t nblk) -> Block16 {
+    alignas(16) uint8_t ring_mem[128];
+    std::memset(ring_mem, 0x5A, sizeof ring_mem);
+    WinRing ring{ring_mem, 0u, 16u};
+    bool ok = scan_doc(blob, blob_tables(blob), d, len, row.data(), ring, [&](uint32_t b, uint32_t nblk) -> Block16 {
         if (b < nblk) return Block16{a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
         return Block16{0, 0, 0, 0};
     });

@@ -67,3 +67,50 @@ def test_fuzz_fast_whitespace_runs(seed):
                 n_fast += 1
                 assert fres == ot, (pats, d)
     assert n_fast > 300
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_fast_long_values_across_windows(seed):
+    """Long keys / values / arrays placed at random offsets so that tokens, key tails and
+    scalars straddle the single-pass scanner's 64-byte windows."""
+    from test_fuzz_lines import _chain, _long_doc
+
+    rng = np.random.default_rng(300 + seed)
+    n_fast = n_all = 0
+    for _ in range(60):
+        pats = FU.rand_patterns(rng, int(rng.integers(1, 6)))
+        nodes, root = _chain(len(pats))
+        rs = O.Ruleset(pats, nodes, root)
+        hr = H.HostRuleset(pats, nodes, root)
+        for _ in range(10):
+            d = _long_doc(rng, pats)
+            ot = [rs.pattern(p, d) for p in range(len(pats))]
+            if O.UNSUPPORTED in ot:
+                continue
+            t_or, _ = rs.matches(d)
+            tf, _, fres = H.eval_fast(hr, d, mis=int(rng.integers(0, 16)))
+            if tf == -2:
+                continue
+            n_all += 1
+            if tf >= 0 and 3 not in fres:
+                n_fast += 1
+                assert fres == ot, (pats, d)
+                assert tf == t_or, (pats, d)
+    assert n_all > 200 and n_fast > 0.4 * n_all, (n_fast, n_all)
+
+
+@pytest.mark.parametrize("workload", ["c1", "c2", "c3"])
+def test_fast_workload_documents(workload):
+    from authorino_amd import workloads as W
+
+    w = W.make(workload, n=300, seed=12)
+    pats, nodes, root = w.expr.flatten()
+    pl = [(p.selector, int(p.operator), p.value) for p in pats]
+    rs = O.Ruleset(pl, nodes, root)
+    hr = H.HostRuleset(pl, nodes, root)
+    for i in range(w.n):
+        d = bytes(w.arena[w.offs[i]:w.offs[i] + w.lens[i]])
+        tf, _, fres = H.eval_fast(hr, d, mis=int(w.offs[i]) % 16)
+        assert tf >= 0, (workload, i)
+        assert fres == [rs.pattern(p, d) for p in range(len(pl))]
+        assert tf == rs.matches(d)[0]
