@@ -72,6 +72,15 @@ struct WinRing {
     AJX_HD uint32_t off(uint32_t a) const { return ((a >> 4) & 7u) * cstride + lane16 + (a & 15u); }
     AJX_HD uint32_t u8(uint32_t a) const { return base[off(a)]; }
     AJX_HD uint32_t u32a(uint32_t a) const { return *reinterpret_cast<const uint32_t*>(base + off(a)); }  // a % 4 == 0
+    AJX_HD uint32_t u32(uint32_t a) const {  // the 4 bytes at a, little-endian
+        const uint32_t q = a & ~3u, sh = a & 3u;
+        const uint32_t w0 = u32a(q), w1 = u32a(q + 4);
+#if defined(__HIP_DEVICE_COMPILE__)
+        return __builtin_amdgcn_alignbyte(w1, w0, sh);
+#else
+        return sh ? (w0 >> (8 * sh)) | (w1 << (32 - 8 * sh)) : w0;
+#endif
+    }
     AJX_HD uint64_t u64(uint32_t a) const {  // the 8 bytes at a, little-endian
         const uint32_t q = a & ~3u, sh = a & 3u;
         const uint32_t w0 = u32a(q), w1 = u32a(q + 4), w2 = u32a(q + 8);
@@ -312,8 +321,17 @@ struct Scan {
             if (slot.sig != sig || (slot.meta & 0xFFFFFFu) != want || klen > 0xFFFFu) continue;
             bool eq = true;
             const uint8_t* kl = lits + slot.key_off;
-            for (uint32_t k = 0; k + 8 < klen; k++)
-                if (d[k0 + k] != kl[k]) { eq = false; break; }
+            const uint32_t a0 = k0 + (wa - (uint32_t)bpos);  // ring position of the key's first byte
+            if (a0 + 64u >= wa) {  // the key began in the ring's windows: compare from LDS
+                for (uint32_t k = 0; k + 8 < klen; k += 4) {
+                    const uint32_t r = klen - 8 - k;
+                    const uint32_t m = r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
+                    if ((ring.u32(a0 + k) ^ load_u32_any(kl + k)) & m) { eq = false; break; }
+                }
+            } else {
+                for (uint32_t k = 0; k + 8 < klen; k++)
+                    if (d[k0 + k] != kl[k]) { eq = false; break; }
+            }
             if (eq) { pending = slot.meta >> 24; return; }
         }
     }
