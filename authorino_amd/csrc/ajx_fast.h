@@ -184,6 +184,7 @@ struct Scan {
     AJX_HD uint32_t value_node() const {
         if (depth == 0) return 0;
         if (!top_is_arr()) return pending;
+        if (!narr) return kNoNode;  // no live array open: the element is off every path
         const uint32_t parent = node_at(depth);
         if (parent == kNoNode || !(tn[parent].flags & 1)) return kNoNode;
         uint32_t h;
@@ -207,7 +208,7 @@ struct Scan {
     }
     // a value (scalar, string or container) inside an array completed: next element
     AJX_HD void element_done() {
-        if (!depth || !top_is_arr()) return;
+        if (!narr || !depth || !top_is_arr()) return;
         const uint32_t a0 = arr0, a1 = arr1;
         const bool h1 = narr >= 2 && (a1 & 0xFF) == depth;
         const bool h0 = !h1 && narr >= 1 && (a0 & 0xFF) == depth;
@@ -216,12 +217,17 @@ struct Scan {
     }
     AJX_HD bool open_container(uint32_t c, uint32_t p) {
         const uint32_t node = value_node();
-        const int32_t s = leaf_sel(node);
         if (depth + 1 >= 63) return false;
         depth++;
-        if (c == '[') is_arr |= 1ull << depth;
-        else is_arr &= ~(1ull << depth);
-        const uint32_t live = (node != kNoNode && tn[node].n_children) ? node : kNoNode;
+        const uint64_t bit = 1ull << depth;
+        is_arr = c == '[' ? is_arr | bit : is_arr & ~bit;
+        if (node == kNoNode) {  // off every selector path (the common case)
+            set_node(depth, kNoNode);
+            st = c == '[' ? X_VALUE_OR_CLOSE : X_KEY_OR_CLOSE;
+            return true;
+        }
+        const int32_t s = leaf_sel(node);
+        const uint32_t live = tn[node].n_children ? node : kNoNode;
         if (live != kNoNode && depth > kFastDepth) return false;
         set_node(depth, live);
         if (s >= 0) {
@@ -247,16 +253,21 @@ struct Scan {
     AJX_HD void close_container(uint32_t p) {
         // (copies first: a conditional over two lvalue members would select their
         // addresses and force the state out of registers)
-        const uint32_t c0 = cap0, c1 = cap1, s0 = cap0_start, s1 = cap1_start, a0 = arr0, a1 = arr1;
-        const uint32_t cs = ncap == 2 ? c1 : c0;
-        if (ncap && (cs >> 8) == depth) {
-            const uint32_t start = ncap == 2 ? s1 : s0;
-            row[1 + (cs & 0xFF)] =
-                (uint64_t)start | ((uint64_t)(((p + 1 - start) & 0xFFFFFFu) | ((uint32_t)T_JSON << 24)) << 32);
-            ncap--;
+        if (ncap) {
+            const uint32_t c0 = cap0, c1 = cap1, s0 = cap0_start, s1 = cap1_start;
+            const uint32_t cs = ncap == 2 ? c1 : c0;
+            if ((cs >> 8) == depth) {
+                const uint32_t start = ncap == 2 ? s1 : s0;
+                row[1 + (cs & 0xFF)] =
+                    (uint64_t)start | ((uint64_t)(((p + 1 - start) & 0xFFFFFFu) | ((uint32_t)T_JSON << 24)) << 32);
+                ncap--;
+            }
         }
-        const uint32_t at = narr == 2 ? a1 : a0;
-        if (narr && (at & 0xFF) == depth) narr--;
+        if (narr) {
+            const uint32_t a0 = arr0, a1 = arr1;
+            const uint32_t at = narr == 2 ? a1 : a0;
+            if ((at & 0xFF) == depth) narr--;
+        }
         depth--;
         st = depth == 0 ? X_DONE : X_COMMA_OR_CLOSE;
         element_done();  // the container was an element of its parent array
@@ -277,8 +288,15 @@ struct Scan {
             c0 = (uint32_t)(t8 >> (8 * (8 - gap_cnt))) & 0xFFu;
             c1 = gap_cnt >= 2 ? (uint32_t)(t8 >> (8 * (9 - gap_cnt))) & 0xFFu : 0u;
         } else {
-            c0 = d[gap_first];
-            c1 = d[gap_first + 1];
+            const uint32_t a0 = gap_first + (wa - (uint32_t)bpos);  // ring position of the first byte
+            if (a0 + 64u >= wa) {
+                const uint32_t w = ring.u32(a0);
+                c0 = w & 0xFFu;
+                c1 = (w >> 8) & 0xFFu;
+            } else {
+                c0 = d[gap_first];
+                c1 = d[gap_first + 1];
+            }
         }
         uint32_t type;
         if (c0 == 't') {
@@ -305,9 +323,13 @@ struct Scan {
     // closing quote of a key at block offset i (doc position p)
     AJX_HD void key_closed(uint32_t p, uint32_t i) {
         pending = kNoNode;
+#ifdef AJX_ABLATE_FAST_NOKEYS
+        return;  // profiling: no selector ever matches (the grammar walk alone)
+#endif
         const uint32_t parent = node_at(depth);
         if (parent == kNoNode) return;
         // (a live node always has children: open_container stores only those)
+        str_open = open_before(i);
         const uint32_t lb = last_bs_before(i);
         if (lb != ~0u && lb > str_open) { st = X_SLOW; return; }  // escaped key on a live path
         const uint32_t k0 = str_open + 1, klen = p - k0;
@@ -342,7 +364,12 @@ struct Scan {
     AJX_HD void token(uint32_t c, uint32_t i) {
         const uint32_t p = (uint32_t)(bpos + (int32_t)i);
         if (gap_cnt) {
+#ifdef AJX_ABLATE_FAST_NOSCALAR
+            st = X_COMMA_OR_CLOSE;
+            if (false) {  // profiling: scalars not validated / recorded
+#else
             if ((st != X_VALUE && st != X_VALUE_OR_CLOSE) || !scalar_value() || (c != ',' && c != ']' && c != '}')) {
+#endif
                 st = X_SLOW;
                 return;
             }
@@ -355,7 +382,6 @@ struct Scan {
             case X_KEY_OR_CLOSE:
             case X_KEY:
                 if (c == '"') {
-                    str_open = open_before(i);
                     st = X_COLON;
                     key_closed(p, i);
                     return;
@@ -369,11 +395,11 @@ struct Scan {
             case X_VALUE:
             case X_VALUE_OR_CLOSE:
                 if (c == '"') {
-                    str_open = open_before(i);
                     const int32_t s = leaf_sel(value_node());
                     if (s >= 0) {
+                        const uint32_t so = open_before(i);
                         const uint32_t lb = last_bs_before(i);
-                        record(s, str_open, p + 1, T_STRING, (lb != ~0u && lb > str_open) ? 1u : 0u);
+                        record(s, so, p + 1, T_STRING, (lb != ~0u && lb > so) ? 1u : 0u);
                     }
                     element_done();
                     st = X_COMMA_OR_CLOSE;
@@ -468,6 +494,19 @@ struct Scan {
             gap_cnt += popc64f(toks) + popc64f(ns);
             return;
         }
+#ifdef AJX_ABLATE_FAST_WALK
+        {  // profiling: iterate the tokens and read each byte, nothing else
+            uint32_t acc = 0;
+            while (toks) {
+                const uint32_t i = ctz64f(toks);
+                toks &= toks - 1;
+                acc += byte_at(i);
+            }
+            gap_cnt += acc & 1u;
+            if (bp + 64 >= (int32_t)n) st = X_DONE;
+            return;
+        }
+#endif
         uint64_t below = 0;  // bits already consumed
         while (toks) {
             const uint32_t i = ctz64f(toks);
