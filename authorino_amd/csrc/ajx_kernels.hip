@@ -137,6 +137,9 @@ constexpr uint32_t kWinRingBytesPerWave = 8 * 64 * 16;
 // single-pass workgroups of up to 8 waves: one LDS copy of the ruleset blob per 8 waves,
 // so blob + rings of 16 waves fit a CU's 160 KiB for blobs up to ~16 KiB (4 waves/SIMD)
 constexpr uint32_t kFastBlock = 512;
+#ifndef AJX_FAST_WAVES
+#define AJX_FAST_WAVES 4  // waves per SIMD the single-pass kernels' register budget is set for
+#endif
 __device__ __forceinline__ WinRing lane_ring(uint32_t ring_off) {
     extern __shared__ uint4 s_dyn_ring[];
     WinRing r;
@@ -189,7 +192,7 @@ __device__ __forceinline__ void finish_request(uint32_t r, const uint8_t* blob, 
 // Stage A alone (profiling split / ablations): structural scan -> capture rows.
 // MODE 1/2 are the loads-only / loads+classification ablations.
 template <int MODE, bool SHARED>
-__global__ __launch_bounds__(kFastBlock, 4) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
+__global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
                                                      const uint32_t* __restrict__ set_of_req,
                                                      const uint8_t* __restrict__ arena,
                                                      const uint64_t* __restrict__ offs,
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(kFastBlock) void ajx_patterns(const uint8_t* const*
 // request's value bytes are still in cache (a separate stage-B launch re-reads them
 // from HBM). Requests stage A can not prove gjson-equivalent go to the slow list.
 template <bool SHARED>
-__global__ __launch_bounds__(kFastBlock, 4) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
+__global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
                                                       const uint32_t* __restrict__ set_of_req,
                                                       const uint8_t* __restrict__ arena,
                                                       const uint64_t* __restrict__ offs,
