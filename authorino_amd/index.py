@@ -1,0 +1,187 @@
+"""Host-side AuthConfig index: per-request AuthConfig selection for multi-tenant batches
+(SURVEY.md §8 a15, config C4).
+
+Restates pkg/index/index.go (the `Index` interface :16-27 and its radix tree :41-260)
+and the `:port` retry of pkg/service/auth.go:270-289. Selection stays on the host, as in
+the reference: the micro-batcher resolves each request's host to an AuthConfig id, and
+the device batch carries that id as `set_of_req` (include/authjx.h).
+
+Keys are hostnames. Each '.' starts a new tree level, read from the TLD down
+(`revertKey`, index.go:252-259). A `*` label matches any host below the longest common
+path between the searched key and the tree; the search climbs from that node to the
+root, taking the first `*` child that holds an entry (`treeNode.get`, index.go:155-177).
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional, Tuple
+
+import numpy as np
+
+KEY_LABELS_SEPARATOR = "."  # index.go:12
+ROOT_KEY_LABEL = ""          # index.go:13
+
+
+class AlreadyExistsError(Exception):
+    """the error `Set` returns for a taken key without override (index.go:183-185)"""
+
+
+class IndexEntry:
+    """index.go:32-35"""
+    __slots__ = ("id", "auth_config")
+
+    def __init__(self, id: str, auth_config):
+        self.id = id
+        self.auth_config = auth_config
+
+
+class _TreeNode:
+    """index.go:139-152"""
+    __slots__ = ("label", "entry", "parent", "children")
+
+    def __init__(self, label: str, parent: Optional["_TreeNode"]):
+        self.label = label
+        self.entry: Optional[IndexEntry] = None
+        self.parent = parent
+        self.children: Dict[str, _TreeNode] = {}
+
+    def longest_common_label(self, key: str) -> Tuple["_TreeNode", str]:
+        """index.go:214-235, iteratively: the deepest node on the key's path, and the
+        labels of the key below it ("" when the key ends at that node)."""
+        labels = key.split(KEY_LABELS_SEPARATOR)
+        if self.label != labels[0]:
+            raise RuntimeError("cannot traverse index tree")  # index.go:222-226 (a panic there)
+        node, i = self, 0
+        while i + 1 < len(labels):
+            child = node.children.get(labels[i + 1])
+            if child is None:
+                break
+            node, i = child, i + 1
+        return node, KEY_LABELS_SEPARATOR.join(labels[i + 1:])
+
+    def get(self, key: str) -> Optional[IndexEntry]:
+        """index.go:155-177"""
+        node, tail = self.longest_common_label(key)
+        if tail == "" and node.entry is not None:  # the longest common node matches the key
+            return node.entry
+        curr = node  # look upwards until the root for a wildcard
+        while True:
+            child = curr.children.get("*")
+            if child is not None and child.entry is not None:
+                return child.entry
+            if curr.parent is None:
+                break
+            curr = curr.parent
+        return None
+
+    def set(self, key: str, entry: IndexEntry, override: bool) -> Optional[Exception]:
+        """index.go:179-212"""
+        target, tail = self.longest_common_label(key)
+        if tail == "":
+            if not override:
+                return AlreadyExistsError("authconfig already exists in the index: %s" % key)
+            target.entry = entry
+            return None
+        labels = tail.split(KEY_LABELS_SEPARATOR)
+        node = _TreeNode(labels[0], target)
+        curr = node
+        for label in labels[1:]:
+            curr.children[label] = _TreeNode(label, curr)
+            curr = curr.children[label]
+        curr.entry = entry
+        target.children[labels[0]] = node
+        return None
+
+    def list(self) -> List[IndexEntry]:
+        """index.go:237-246"""
+        out, stack = [], [self]
+        while stack:
+            n = stack.pop()
+            if n.entry is not None:
+                out.append(n.entry)
+            stack.extend(reversed(list(n.children.values())))
+        return out
+
+
+def revert_key(key: str) -> str:
+    """index.go:252-259: "talker-api.nip.io" -> ".io.nip.talker-api" (root label first)"""
+    labels = key.split(KEY_LABELS_SEPARATOR) + [ROOT_KEY_LABEL]
+    return KEY_LABELS_SEPARATOR.join(reversed(labels))
+
+
+class Index:
+    """`index.NewIndex()` (index.go:28-30): the AuthConfig tree (authConfigTree, :41-137).
+    Errors are returned, as the Go methods do, rather than raised."""
+
+    def __init__(self):
+        self._root = _TreeNode(ROOT_KEY_LABEL, None)
+        self._keys: Dict[str, List[str]] = {}
+
+    def get(self, key: str):
+        """index.go:56-65: the AuthConfig for a host, or None"""
+        e = self._root.get(revert_key(key))
+        return e.auth_config if e is not None else None
+
+    def set(self, id: str, key: str, config, override: bool = False) -> Optional[Exception]:
+        """index.go:67-80"""
+        err = self._root.set(revert_key(key), IndexEntry(id, config), override)
+        if err is None:
+            self._keys.setdefault(id, []).append(key)
+        return err
+
+    def delete(self, id: str) -> None:
+        """index.go:82-91"""
+        for key in self._keys.get(id, []):
+            self._delete_key(id, key)
+
+    def delete_key(self, id: str, key: str) -> None:
+        """index.go:93-98"""
+        self._delete_key(id, key)
+
+    def list(self) -> list:
+        """index.go:100-109"""
+        return [e.auth_config for e in self._root.list()]
+
+    def empty(self) -> bool:
+        """index.go:111-113"""
+        return len(self._keys) == 0
+
+    def find_id(self, key: str) -> Tuple[str, bool]:
+        """index.go:115-123"""
+        e = self._root.get(revert_key(key))
+        return (e.id, True) if e is not None else ("", False)
+
+    def find_keys(self, id: str) -> Optional[List[str]]:
+        """index.go:125-130"""
+        return self._keys.get(id)
+
+    def _delete_key(self, id: str, key: str) -> None:
+        """index.go:132-136 (the keys map keeps the id, as in the reference)"""
+        node, _ = self._root.longest_common_label(revert_key(key))
+        if node is not None and node.entry is not None and node.entry.id == id:
+            node.entry = None
+
+
+def lookup(index: Index, host: str):
+    """pkg/service/auth.go:270-280: Index.Get(host); when not found and the host has a
+    port, retry with the part before the first ':'"""
+    cfg = index.get(host)
+    if cfg is None and ":" in host:
+        cfg = index.get(host.split(":")[0])
+    return cfg
+
+
+def select_sets(index: Index, hosts: Iterable[str], not_found: int = -1) -> np.ndarray:
+    """The micro-batcher's selection step for a batch: `lookup` per request, each distinct
+    host resolved once. The index's configs are set ids (ints) here; requests whose host
+    resolves to nothing get `not_found` (the reference answers NOT_FOUND, auth.go:282-287,
+    without evaluating anything)."""
+    memo: Dict[str, int] = {}
+    hosts = list(hosts)
+    out = np.empty(len(hosts), dtype=np.int64)
+    for i, h in enumerate(hosts):
+        v = memo.get(h)
+        if v is None:
+            cfg = lookup(index, h)
+            v = memo[h] = not_found if cfg is None else int(cfg)
+        out[i] = v
+    return out

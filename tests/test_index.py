@@ -1,0 +1,87 @@
+"""Host AuthConfig index (authorino_amd/index.py) against the reference's own test,
+pkg/index/index_test.go:38-140 (TestAuthConfigTree), plus the `:port` retry of
+pkg/service/auth.go:270-280 and wildcard climbing from deeper keys."""
+import numpy as np
+
+from authorino_amd import index as ix
+
+
+def test_auth_config_tree():
+    """index_test.go:38-140, step by step (configs are plain markers here)"""
+    c = ix.Index()
+    ac1, ac2, ac3, ac4 = "cfg-1", "cfg-2", "cfg-3", "cfg-4"
+    assert c.set("auth-1", "*.io", ac1, False) is None  # the more generic host first
+    assert c.set("auth-2", "talker-api.nip.io", ac2, False) is None  # ...then the more specific one
+    assert c.set("auth-2", "*.pets.com", ac2, False) is None
+    assert c.set("auth-3", "api.acme.com", ac3, False) is None  # the more specific host first
+    assert c.set("auth-4", "*.acme.com", ac4, False) is None  # ...then the more generic one
+
+    assert sorted(c.find_keys("auth-1")) == ["*.io"]
+    assert sorted(c.find_keys("auth-2")) == ["*.pets.com", "talker-api.nip.io"]
+    assert c.find_keys("auth-x") is None
+
+    assert c.find_id("*.pets.com") == ("auth-2", True)
+    assert c.find_id("talker-api.nip.io") == ("auth-2", True)
+    assert c.find_id("*.acme.com") == ("auth-4", True)
+    assert c.find_id("undefined.com") == ("", False)
+
+    err = c.set("auth-5", "talker-api.nip.io", "cfg-5", False)  # same host, no override
+    assert isinstance(err, ix.AlreadyExistsError)
+    # (treeNode.set formats the reverted key it was handed, index.go:71,184)
+    assert str(err) == "authconfig already exists in the index: .io.nip.talker-api"
+
+    assert c.get("dogs.pets.com") == ac2
+    assert c.get("api.acme.com") == ac3
+    assert c.get("www.acme.com") == ac4
+    assert c.get("talker-api.nip.io") == ac2
+    assert c.get("foo.nip.io") == ac1
+    assert c.get("foo.org") is None
+
+    c.delete("auth-2")  # all entries of the id go
+    assert c.get("dogs.pets.com") is None
+    assert c.get("talker-api.nip.io") == ac1  # `*.io <- auth-1` is still in the tree
+    assert c.get("api.acme.com") == ac3
+
+    c.delete("auth-3")
+    assert c.get("api.acme.com") == ac4  # `*.acme.com <- auth-4` is still in the tree
+
+
+def test_override_list_and_empty():
+    c = ix.Index()
+    assert c.empty()
+    assert c.set("a", "x.example.com", 1) is None
+    assert c.set("b", "x.example.com", 2, True) is None  # override replaces the entry
+    assert c.get("x.example.com") == 2
+    assert sorted(c.list()) == [2]
+    assert not c.empty()
+    c.delete_key("a", "x.example.com")  # not a's entry any more: stays
+    assert c.get("x.example.com") == 2
+    c.delete_key("b", "x.example.com")
+    assert c.get("x.example.com") is None
+
+
+def test_wildcard_climbs_from_the_longest_common_path():
+    c = ix.Index()
+    c.set("root-wild", "*.com", 1)
+    c.set("deep", "a.b.example.com", 2)
+    c.set("mid-wild", "*.example.com", 3)
+    assert c.get("a.b.example.com") == 2
+    assert c.get("z.b.example.com") == 3   # b.example.com has no entry: climb to *.example.com
+    assert c.get("b.example.com") == 3     # an interior node without entry: climb
+    assert c.get("q.other.com") == 1
+    assert c.get("example.org") is None
+    assert ix.revert_key("talker-api.nip.io") == ".io.nip.talker-api"
+
+
+def test_port_retry_and_batch_selection():
+    """auth.go:270-280: a host with a port is retried without it"""
+    c = ix.Index()
+    c.set("t1", "t1.example.com", 0)
+    c.set("t2", "t2.example.com:8080", 1)  # a key with a port matches only with it
+    c.set("w", "*.r0.example.com", 2)
+    assert ix.lookup(c, "t1.example.com:443") == 0
+    assert ix.lookup(c, "t2.example.com:8080") == 1
+    assert ix.lookup(c, "t2.example.com") is None
+    assert ix.lookup(c, "api.r0.example.com:443") == 2
+    sel = ix.select_sets(c, ["t1.example.com", "x.r0.example.com", "nope.example.net", "t1.example.com:1"])
+    assert sel.dtype == np.int64 and sel.tolist() == [0, 2, -1, 0]
