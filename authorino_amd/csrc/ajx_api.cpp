@@ -219,6 +219,72 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     return AUTHJX_OK;
 }
 
+static_assert(sizeof(authjx_value) == 12, "authjx_value is three u32 words on the device");
+
+int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                               const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
+                               const uint32_t* d_lens, uint32_t n, authjx_value* d_out_values,
+                               uint32_t values_stride, void* stream) {
+    if (!ctx || !sets || n_sets == 0 || (n && (!d_arena || !d_offs || !d_lens || !d_out_values)))
+        return AUTHJX_EINVAL;
+    if (n_sets > 1 && !d_set_of_req) return AUTHJX_EINVAL;
+    if (n_sets == 1) d_set_of_req = nullptr;
+    for (uint32_t i = 0; i < n_sets; i++)
+        if (!sets[i] || sets[i]->c.n_patterns > values_stride) return AUTHJX_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_OK(hipSetDevice(ctx->device));
+    int rc = ensure_sets(ctx, sets, n_sets, s);
+    if (rc != AUTHJX_OK) return rc;
+    HIP_OK(ajx::launch_select(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n,
+                              reinterpret_cast<uint32_t*>(d_out_values), values_stride, s));
+    return AUTHJX_OK;
+}
+
+int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                        const uint32_t* set_of_req, const uint8_t* arena, uint64_t arena_len,
+                        const uint64_t* offs, const uint32_t* lens, uint32_t n, authjx_value* out_values,
+                        uint32_t values_stride) {
+    if (!ctx || (n && (!arena || !offs || !lens || !out_values))) return AUTHJX_EINVAL;
+    for (uint32_t r = 0; r < n; r++)
+        if (offs[r] + lens[r] > arena_len) return AUTHJX_EINVAL;
+    const bool with_sor = set_of_req != nullptr;
+    const size_t o_offs = round_up(arena_len, 256);
+    const size_t o_lens = round_up(o_offs + (size_t)n * 8, 256);
+    const size_t o_sor = round_up(o_lens + (size_t)n * 4, 256);
+    const size_t o_out = round_up(o_sor + (with_sor ? (size_t)n * 4 : 0), 256);
+    const size_t out_bytes = (size_t)n * values_stride * sizeof(authjx_value);
+    const size_t total = round_up(o_out + out_bytes, 256);
+    std::lock_guard<std::mutex> batch_lock(ctx->batch_mu);
+    {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        HIP_OK(hipSetDevice(ctx->device));
+        if (total > ctx->stage_cap) {
+            HIP_OK(hipStreamSynchronize(ctx->stream));
+            if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+            ctx->d_stage = nullptr;
+            ctx->stage_cap = 0;
+            HIP_OK(hipMalloc(&ctx->d_stage, total));
+            ctx->stage_cap = total;
+        }
+        uint8_t* b = ctx->d_stage;
+        hipStream_t s = ctx->stream;
+        HIP_OK(hipMemcpyAsync(b, arena, arena_len, hipMemcpyHostToDevice, s));
+        HIP_OK(hipMemcpyAsync(b + o_offs, offs, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        HIP_OK(hipMemcpyAsync(b + o_lens, lens, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        if (with_sor) HIP_OK(hipMemcpyAsync(b + o_sor, set_of_req, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    }
+    uint8_t* b = ctx->d_stage;
+    int rc = authjx_select_batch_device(ctx, sets, n_sets, with_sor ? (const uint32_t*)(b + o_sor) : nullptr, b,
+                                        (const uint64_t*)(b + o_offs), (const uint32_t*)(b + o_lens), n,
+                                        (authjx_value*)(b + o_out), values_stride, nullptr);
+    if (rc != AUTHJX_OK) return rc;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    HIP_OK(hipMemcpyAsync(out_values, b + o_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    return AUTHJX_OK;
+}
+
 // Profiling only (not in authjx.h): replace stage A by a reduced variant whose outputs
 // are meaningless, to price its parts (loads, classification) on the hardware.
 int authjx_debug_ablate(authjx_ctx* ctx, int mode) {

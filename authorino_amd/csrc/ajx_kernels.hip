@@ -356,6 +356,54 @@ __global__ __launch_bounds__(kLinesBlock, AJX_LINES_WAVES) void ajx_scan_lines(
     if (out_err) out_err[r] = ep;
 }
 
+// gjson.Get per pattern selector (the response / header selectors of SURVEY.md §8 a14):
+// one work-item per request, the exact device Get (gj_get) for each of the ruleset's
+// patterns; out[r * stride + p] = {start (relative to the document), len, type, esc}.
+// An UNSUPPORTED selector reports type 0xFF.
+__global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* __restrict__ sets,
+                                                         const uint32_t* __restrict__ set_of_req,
+                                                         const uint8_t* __restrict__ arena,
+                                                         const uint64_t* __restrict__ offs,
+                                                         const uint32_t* __restrict__ lens, uint32_t n,
+                                                         uint32_t* __restrict__ out, uint32_t stride) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    const Selector* sels = reinterpret_cast<const Selector*>(blob + h->off_selectors);
+    const Component* comps = reinterpret_cast<const Component*>(blob + h->off_components);
+    const Pattern* pats = reinterpret_cast<const Pattern*>(blob + h->off_patterns);
+    const uint8_t* lits = blob + h->off_literals;
+    const uint8_t* doc = arena + offs[r];
+    const uint32_t len = lens[r];
+    const uint32_t np = h->n_patterns < stride ? h->n_patterns : stride;
+    for (uint32_t p = 0; p < np; p++) {
+        uint32_t* o = out + ((size_t)r * stride + p) * 3;
+        if (pats[p].state == P_UNSUPPORTED) {
+            o[0] = 0;
+            o[1] = 0;
+            o[2] = 0xFFu;
+            continue;
+        }
+        const Selector& sl = sels[pats[p].selector];
+        const ValueRef v = gj_get(doc, len, comps + sl.comp_begin, sl.comp_count, lits);
+        o[0] = v.start;
+        o[1] = v.end - v.start;
+        o[2] = (uint32_t)v.type | ((uint32_t)v.esc << 8);
+    }
+}
+
+hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
+                         const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint32_t* d_out,
+                         uint32_t stride, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t block = 256;
+    const uint32_t grid = (n + block - 1) / block;
+    hipLaunchKernelGGL(ajx_select_values, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
+                       d_lens, n, d_out, stride);
+    return hipGetLastError();
+}
+
 hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
                             const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
                             int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream) {

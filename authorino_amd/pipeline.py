@@ -10,6 +10,12 @@ the `when` gates and the authorization phase, batched over many requests.
                                    priority evaluated, the first failure is PERMISSION_DENIED
                                    (:478-481); a success stores the object under
                                    auth.authorization.<name> for later priorities (:312).
+  response phase                   auth_pipeline.go:324-349 + :490-494 (only after a
+                                   successful authorization phase): per priority, each
+                                   response config's `when`, then Plain / DynamicJSON
+                                   objects wrapped as headers (evaluators.WrapResponses,
+                                   pkg/evaluators/response.go:150-174). Selector lookups
+                                   run on the device (authorino_amd.response).
 
 AuthPipelineBatch compiles every expression once (the reconcile-time compile point,
 controllers/auth_config_controller.go) and evaluates each priority level of a batch in ONE
@@ -32,6 +38,7 @@ import numpy as np
 
 from . import jsonexp
 from .authorization import JSONPatternMatching, UnauthorizedError
+from .response import ResponseConfig, ResponseSelectors, wrap_responses
 
 UNMATCHING_CONDITIONS = "unmatching conditions for config"
 CODE_OK = 0  # rpc.OK
@@ -74,6 +81,7 @@ class AuthConfig:
 
     conditions: Optional[jsonexp.Expression] = None  # AuthConfig-level `when`
     authorization: List[AuthorizationConfig] = field(default_factory=list)
+    response: List[ResponseConfig] = field(default_factory=list)
 
 
 @dataclass
@@ -85,6 +93,8 @@ class AuthResult:
     skipped: bool = False  # AuthConfig-level conditions not met (auth_pipeline.go:454-457)
     denied_by: Optional[str] = None
     authorization: Dict[str, object] = field(default_factory=dict)
+    headers: Dict[str, str] = field(default_factory=dict)      # success: WrapResponses headers
+    metadata: Dict[str, object] = field(default_factory=dict)  # success: dynamic metadata
 
 
 def _selects_authorization(expr: Optional[jsonexp.Expression]) -> bool:
@@ -104,6 +114,7 @@ class AuthPipelineBatch:
         self.ctx = ctx if ctx is not None else runtime.context(device)
         self._rs: Dict[int, object] = {}
         exprs = [auth_config.conditions] + [e for c in auth_config.authorization for e in (c.conditions, c.rules)]
+        exprs += [c.conditions for c in auth_config.response]
         for e in exprs:
             if e is not None and id(e) not in self._rs:
                 self._rs[id(e)] = self.ctx.compile_expression(e)
@@ -111,6 +122,13 @@ class AuthPipelineBatch:
         self.levels = [[c for c in auth_config.authorization if c.priority == p] for p in prios]
         self._needs_regen = any(_selects_authorization(e) for lvl in self.levels[1:] for c in lvl
                                 for e in (c.conditions, c.rules))
+        rprios = sorted({c.priority for c in auth_config.response})
+        self.response_levels = [[c for c in auth_config.response if c.priority == p] for p in rprios]
+        self.selectors = ResponseSelectors(auth_config.response, self.ctx) if auth_config.response else None
+        for c in auth_config.response:
+            for v in c.values():
+                if any(p.startswith("auth.authorization") or p.startswith("auth.response") for p in v.paths()):
+                    raise ValueError("response selectors over auth.authorization/auth.response are not batched")
 
     # one launch: expression k of `exprs` on every request in `reqs`
     def _eval(self, exprs: Sequence[jsonexp.Expression], reqs: np.ndarray, arena, offs, lens):
@@ -193,7 +211,37 @@ class AuthPipelineBatch:
                         else:
                             res.message = str(UnauthorizedError())
             live = live[~denied]
+        if self.selectors is not None and len(live):
+            self._responses(results, docs, live)
         return results
+
+    def _responses(self, results, docs, live):
+        """Phase 4 for the requests that passed authorization (auth_pipeline.go:490-494)."""
+        from . import runtime
+
+        sub = [docs[i] for i in live.tolist()]
+        lens = np.fromiter((len(d) for d in sub), dtype=np.uint32, count=len(sub))
+        offs = np.zeros(len(sub), dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        arena = np.frombuffer(b"".join(sub) + b"\0", dtype=np.uint8)
+        spans = self.selectors.resolve(sub, arena, offs, lens)
+        if spans.size and ((spans[:, :, 2] & 0xFF) == 255).any():
+            raise runtime.AuthjxError("device could not resolve a response selector")
+        granted = [dict() for _ in sub]
+        idx = np.arange(len(sub))
+        for level in self.response_levels:
+            conds = [c.conditions for c in level if c.conditions is not None]
+            met = {}
+            if conds:
+                tri, _, _ = self._eval(conds, idx, arena, offs, lens)
+                met = {id(e): tri[j] == runtime.T for j, e in enumerate(conds)}
+            for c in level:
+                ok = met[id(c.conditions)] if c.conditions is not None else None
+                for j in range(len(sub)):
+                    if ok is None or ok[j]:
+                        granted[j][c.name] = (c, self.selectors.call(c, sub[j], spans[j]))
+        for j, i in enumerate(live.tolist()):
+            results[i].headers, results[i].metadata = wrap_responses(granted[j])
 
 
 def evaluate_json_authorization(rules: Optional[jsonexp.Expression], docs: Sequence):

@@ -48,7 +48,7 @@ EXPORTS = [
     "authjx_init", "authjx_shutdown", "authjx_device_count", "authjx_compile", "authjx_free",
     "authjx_ruleset_patterns", "authjx_ruleset_selectors", "authjx_pattern_error",
     "authjx_eval_batch_device", "authjx_eval_batch", "authjx_last_kernel_ms", "authjx_set_exact_scan",
-    "authjx_last_exact_count",
+    "authjx_last_exact_count", "authjx_select_batch_device", "authjx_select_batch",
 ]
 
 
@@ -93,6 +93,14 @@ def load_library(path: str = LIB_PATH):
             C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
             C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
         L.authjx_eval_batch.restype = C.c_int
+        L.authjx_select_batch_device.argtypes = [
+            C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+            C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
+        L.authjx_select_batch_device.restype = C.c_int
+        L.authjx_select_batch.argtypes = [
+            C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+            C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+        L.authjx_select_batch.restype = C.c_int
         L.authjx_last_kernel_ms.argtypes = [C.c_void_p]
         L.authjx_last_kernel_ms.restype = C.c_float
         L.authjx_set_exact_scan.argtypes = [C.c_void_p, C.c_int]
@@ -195,6 +203,28 @@ class Context:
             words if bm is not None else 0)
         _check(rc, "authjx_eval_batch")
         return tri[:n], err[:n], (bm[:n] if bm is not None else None)
+
+    def select_host_arena(self, sets, arena, offs, lens, set_of_req=None) -> np.ndarray:
+        """gjson.Get of every pattern selector of each request's ruleset on the device
+        (authjx_select_batch): u32[n][stride][3] = {start, len, type | esc << 8}."""
+        n = int(lens.shape[0])
+        stride = max(1, max(s.n_patterns for s in sets))
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        if arena.nbytes == 0:
+            arena = np.zeros(1, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.zeros((max(n, 1), stride, 3), dtype=np.uint32)
+        sor = None
+        if set_of_req is not None:
+            set_of_req = np.ascontiguousarray(set_of_req, dtype=np.uint32)
+            sor = C.c_void_p(set_of_req.ctypes.data)
+        sarr = (C.c_void_p * len(sets))(*[s._h.value for s in sets])
+        rc = load_library().authjx_select_batch(
+            self._h, sarr, len(sets), sor, C.c_void_p(arena.ctypes.data), int(arena.nbytes),
+            C.c_void_p(offs.ctypes.data), C.c_void_p(lens.ctypes.data), n, C.c_void_p(out.ctypes.data), stride)
+        _check(rc, "authjx_select_batch")
+        return out[:n]
 
     def close(self):
         if getattr(self, "_h", None):

@@ -10,6 +10,12 @@ No dataset is fetched: everything is generated from numpy default_rng(seed).
   c2  N docs of 768..1280 B, one All of 16 eq/neq/incl patterns over 12 selectors
   c3  N docs, 64 patterns (24 eq, 12 neq, 10 incl, 10 excl, 8 matches),
       All(Any x4 of 8, All x4 of 8)
+  c4  N docs x 10k multi-tenant AuthConfigs (8-32 patterns each, regex in 10 %), each
+      request's AuthConfig selected on the host through the pkg/index restatement from a
+      Zipf(1.1) request host; requests bucketed by AuthConfig (set_of_req sorted)
+  c5  N JWT-claims-heavy docs of 4096 +- 64 B, one AuthConfig with the full authz phase:
+      4 top-level `when`, 4 authz configs (2 `when` + 16 rules each, 2 `matches`), 4
+      response header selectors (2 plain, 2 json)
 """
 from __future__ import annotations
 
@@ -41,8 +47,16 @@ class Workload:
     arena: np.ndarray  # uint8
     offs: np.ndarray   # uint64
     lens: np.ndarray   # uint32
-    expr: object       # jsonexp.Expression
+    expr: object       # jsonexp.Expression (the first AuthConfig's, for multi-tenant batches)
     description: str
+    exprs: Optional[list] = None          # multi-tenant: one expression per AuthConfig (set id)
+    set_of_req: Optional[np.ndarray] = None  # multi-tenant: u32[n] set id per request
+    hosts: Optional[List[str]] = None     # multi-tenant: request host per request (index input)
+    auth_config: object = None            # c5: the pipeline.AuthConfig of the full phase
+
+    @property
+    def sets(self) -> list:
+        return self.exprs if self.exprs is not None else [self.expr]
 
     @property
     def n(self) -> int:
@@ -51,6 +65,13 @@ class Workload:
     @property
     def n_patterns(self) -> int:
         return len(self.expr.flatten()[0])
+
+    def patterns_per_request(self) -> np.ndarray:
+        """R of each request's selected rule set (request x rule evaluations per request)."""
+        counts = np.array([len(e.flatten()[0]) for e in self.sets], dtype=np.int64)
+        if self.set_of_req is None:
+            return np.full(self.n, counts[0], dtype=np.int64)
+        return counts[self.set_of_req]
 
     def doc(self, i: int) -> bytes:
         o = int(self.offs[i])
@@ -144,12 +165,53 @@ def _make_doc(rng: np.random.Generator, target_len: int, uid: int) -> bytes:
     return s.encode("utf-8")
 
 
-def make_docs(n: int, seed: int, lo: int = 768, hi: int = 1280, unique: int = 4096) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+C5_GROUPS = ["grp-%02d" % i for i in range(64)]
+C5_ROLES = ["role-%02d" % i for i in range(40)]
+
+
+def _make_doc_c5(rng: np.random.Generator, target_len: int, uid: int) -> bytes:
+    """A JWT-claims-heavy Authorization JSON (~4 KiB): the c2 document plus 32 groups, 20
+    realm roles and nested resource_access client roles in the identity."""
+    base = json.loads(_make_doc(rng, 900, uid))
+    ident = base["auth"]["identity"]
+    groups = sorted(set(rng.choice(C5_GROUPS, size=31, replace=False).tolist()) | {"users"})
+    if rng.random() < 0.05:
+        groups = [g for g in groups if g != "users"]
+    ident["groups"] = groups
+    ident["realm_access"] = {"roles": sorted(set(rng.choice(C5_ROLES, size=19, replace=False).tolist()) | {"reader"})}
+    ident["resource_access"] = go_map({
+        "talker-api": {"roles": sorted(rng.choice(["read", "write", "admin", "audit"], size=2, replace=False).tolist())},
+        "account": {"roles": ["manage-account", "view-profile"]},
+        "billing-%d" % int(rng.integers(0, 9)): {"roles": ["viewer"]},
+    })
+    ident["session_state"] = _hex(rng, 32)
+    ident["sid"] = _hex(rng, 32)
+    ident["jti"] = _hex(rng, 24)
+    ident["auth_time"] = int(1699990000 + rng.integers(0, 10**6))
+    ident["given_name"] = "User"
+    ident["family_name"] = str(uid)
+    base["auth"]["identity"] = go_map(ident)
+    s = go_json(base)
+    # the rest is the bearer token itself (a signed JWT of these claims is this long)
+    short = target_len - len(s)
+    if short > 0:
+        hdrs = base["context"]["request"]["http"]["headers"]
+        b64 = np.array(list("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_"))
+        tok = hdrs["authorization"][len("Bearer "):]
+        extra = "".join(rng.choice(b64, size=short).tolist())
+        hdrs["authorization"] = "Bearer eyJ" + extra[:max(0, short - 3)] + tok
+        s = go_json(base)
+    return s.encode("utf-8")
+
+
+def make_docs(n: int, seed: int, lo: int = 768, hi: int = 1280, unique: int = 4096,
+              maker=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     """n documents (lengths ~U[lo, hi]) packed into (arena, offs, lens). `unique` distinct
     documents are generated and tiled by a random permutation."""
     rng = np.random.default_rng(seed)
     m = min(n, unique)
-    base = [_make_doc(rng, int(rng.integers(lo, hi + 1)), i) for i in range(m)]
+    maker = maker or _make_doc
+    base = [maker(rng, int(rng.integers(lo, hi + 1)), i) for i in range(m)]
     idx = rng.integers(0, m, size=n) if n > m else np.arange(n)
     parts = [base[i] for i in idx]
     lens = np.fromiter((len(b) for b in parts), dtype=np.uint32, count=n)
@@ -253,6 +315,153 @@ def c3_expression():
     return All(*[Any(*g) for g in any_groups], *[All(*g) for g in all_groups])
 
 
+def _c4_pattern_pool():
+    """(selector, operator, value) candidates for the multi-tenant rule sets: the c3 pools
+    plus per-tenant literals."""
+    e = c3_expression()
+    pats, _, _ = e.flatten()
+    plain = [(p.selector, p.operator, p.value) for p in pats if p.operator != RegexOperator]
+    rx = [(p.selector, p.operator, p.value) for p in pats if p.operator == RegexOperator]
+    return plain, rx
+
+
+def c4_expression(rng: np.random.Generator, tenant: int, plain, rx):
+    """One tenant's AuthConfig rules: 8-32 patterns (1-2 `matches` in 10 % of the configs)
+    in a random two- or three-level All/Any tree."""
+    k = int(rng.integers(8, 33))
+    n_rx = int(rng.integers(1, 3)) if rng.random() < 0.10 else 0
+    chosen = [plain[i] for i in rng.choice(len(plain), size=k - n_rx, replace=True)]
+    chosen += [rx[i] for i in rng.choice(len(rx), size=n_rx, replace=False)]
+    # per-tenant literals so that no two configs are the same
+    extra = [("auth.identity.sub", NotEqualOperator, "user-%04d" % (tenant % 9973)),
+             ("context.request.http.headers.x-tenant", NotEqualOperator, "t%d" % tenant)]
+    chosen[:2] = extra
+    pats = [Pattern(sel, op, val) for sel, op, val in chosen]
+    pats = [pats[i] for i in rng.permutation(len(pats))]
+    groups, i = [], 0
+    while i < len(pats):
+        g = int(rng.integers(2, 9))
+        grp = pats[i:i + g]
+        i += g
+        node = Any(*grp) if rng.random() < 0.3 else All(*grp)
+        if rng.random() < 0.2 and len(groups) > 0:  # a third level
+            node = All(groups.pop(), node) if rng.random() < 0.5 else Any(groups.pop(), node)
+        groups.append(node)
+    return All(*groups)
+
+
+def c4_index_and_rules(n_configs: int = 10000, n_wild: int = 100, seed: int = 4):
+    """The AuthConfigs: hosts t<i>.example.com (i < n_configs - n_wild) and wildcards
+    *.r<j>.example.com, in a pkg/index restatement whose entries are set ids."""
+    from .index import Index
+
+    rng = np.random.default_rng(seed)
+    plain, rx = _c4_pattern_pool()
+    idx = Index()
+    exprs = []
+    n_exact = n_configs - n_wild
+    for i in range(n_configs):
+        host = "t%d.example.com" % i if i < n_exact else "*.r%d.example.com" % (i - n_exact)
+        err = idx.set("ns/cfg-%d" % i, host, i, False)
+        assert err is None, err
+        exprs.append(c4_expression(rng, i, plain, rx))
+    return idx, exprs
+
+
+def c4_hosts(n: int, n_configs: int, n_wild: int, rng: np.random.Generator) -> List[str]:
+    """Request hosts: 85 % exact tenant hosts and 10 % wildcard hits, both Zipf(1.1) over
+    tenants; 3 % carry a :port (the auth.go:270-289 retry); 2 % match no AuthConfig."""
+    n_exact = n_configs - n_wild
+    def zipf(m, size):
+        w = 1.0 / np.arange(1, m + 1) ** 1.1
+        return rng.choice(m, size=size, p=w / w.sum())
+    kind = rng.random(n)
+    ex = zipf(n_exact, n)
+    wi = zipf(n_wild, n)
+    sub = rng.integers(0, 1000, size=n)
+    hosts = []
+    for i in range(n):
+        if kind[i] < 0.85:
+            h = "t%d.example.com" % ex[i]
+        elif kind[i] < 0.95:
+            h = "h%d.r%d.example.com" % (sub[i], wi[i])
+        elif kind[i] < 0.98:
+            h = "t%d.example.com:8443" % ex[i]
+        else:
+            h = "u%d.nowhere.io" % sub[i]
+        hosts.append(h)
+    return hosts
+
+
+def make_c4(n: int, seed: int = 4, n_configs: int = 10000, n_wild: int = 100) -> Workload:
+    """C4: multi-tenant batch. Each request's AuthConfig comes from the
+    host index (requests without one are dropped, as the reference answers NOT_FOUND
+    before any evaluation); the batch is bucketed by AuthConfig. Document bodies are the
+    c2 generator's (Authorization JSON of ~1 KiB)."""
+    from .index import select_sets
+
+    idx, exprs = c4_index_and_rules(n_configs, n_wild, seed=4)
+    rng = np.random.default_rng(seed)
+    m = int(n * 1.03) + 16
+    hosts = c4_hosts(m, n_configs, n_wild, rng)
+    sets = select_sets(idx, hosts)
+    keep = np.nonzero(sets >= 0)[0][:n]
+    sets = sets[keep]
+    order = np.argsort(sets, kind="stable")  # bucket by AuthConfig
+    arena, offs, lens = make_docs(len(keep), seed)
+    return Workload("c4", arena, offs[order], lens[order], exprs[0],
+                    f"{len(keep)} docs x {n_configs} AuthConfigs (8-32 patterns, regex in 10 %), "
+                    "host-index selection, bucketed by AuthConfig",
+                    exprs=exprs, set_of_req=sets[order].astype(np.uint32),
+                    hosts=[hosts[keep[i]] for i in order])
+
+
+def c5_auth_config():
+    """C5's AuthConfig: top-level `when` of 4 patterns; 4 authorization
+    configs, each with a 2-pattern `when` and 16 rules (2 `matches`); 4 response header
+    selectors (2 plain, 2 DynamicJSON, one with a template)."""
+    from .pipeline import AuthConfig, AuthorizationConfig
+    from .response import JSONValue, ResponseConfig
+
+    P = Pattern
+    top = All(P("context.request.http.method", NotEqualOperator, "DELETE"),
+              P("context.request.http.host", EqualOperator, "api.example.com"),
+              P("context.request.http.path", RegexOperator, r"^/(api|admin)/"),
+              P("context.request.http.headers.x-tenant", EqualOperator, "acme"))
+    authz = []
+    for k in range(4):
+        g = ["grp-%02d" % ((7 * k + j) % 64) for j in range(4)]
+        r = ["role-%02d" % ((5 * k + j) % 40) for j in range(4)]
+        cond = All(P("context.request.http.scheme", EqualOperator, "https"),
+                   P("auth.identity.aud", EqualOperator, "talker-api") if k % 2 == 0
+                   else P("auth.identity.azp", NotEqualOperator, "other"))
+        rules = All(
+            P("auth.identity.iss", EqualOperator, "https://sso.example.com/realms/acme"),
+            P("auth.identity.email_verified", EqualOperator, "true"),
+            P("auth.identity.groups", IncludesOperator, "users"),
+            P("auth.identity.realm_access.roles", IncludesOperator, "reader"),
+            Any(*[P("auth.identity.groups", IncludesOperator, x) for x in g]),
+            Any(*[P("auth.identity.realm_access.roles", IncludesOperator, x) for x in r]),
+            P("auth.identity.groups", ExcludesOperator, "banned"),
+            P("auth.identity.sub", NotEqualOperator, "user-0000"),
+            P("auth.identity.email", RegexOperator, r"@example\.com$"),
+            P("auth.identity.preferred_username", RegexOperator, r"^user-\d{4}$"))
+        authz.append(AuthorizationConfig("authz-%d" % k, rules=rules, conditions=cond, priority=0))
+    resp = [
+        ResponseConfig("user", plain=JSONValue(pattern="auth.identity.sub"), wrapper_key="x-auth-user"),
+        ResponseConfig("exp", plain=JSONValue(pattern="auth.identity.exp"), wrapper_key="x-auth-exp"),
+        ResponseConfig("claims", json_properties=[("groups", JSONValue(pattern="auth.identity.realm_access.roles")),
+                                                  ("tenant", JSONValue(pattern="auth.metadata.tenant")),
+                                                  ("acr", JSONValue(pattern="auth.identity.acr"))],
+                       wrapper_key="x-auth-claims"),
+        ResponseConfig("ctx", json_properties=[
+            ("user", JSONValue(pattern="{auth.identity.preferred_username}@{context.request.http.host}")),
+            ("client_roles", JSONValue(pattern="auth.identity.resource_access.talker-api.roles")),
+            ("static", JSONValue(static="v1"))], wrapper_key="x-auth-ctx"),
+    ]
+    return AuthConfig(conditions=top, authorization=authz, response=resp)
+
+
 def make(name: str, n: Optional[int] = None, seed: Optional[int] = None) -> Workload:
     name = name.lower()
     if name == "c1":
@@ -268,4 +477,13 @@ def make(name: str, n: Optional[int] = None, seed: Optional[int] = None) -> Work
         arena, offs, lens = make_docs(n, seed if seed is not None else 3)
         return Workload("c3", arena, offs, lens, c3_expression(),
                         f"{n} docs x 64 patterns (24 eq/12 neq/10 incl/10 excl/8 matches), All(Any x4, All x4)")
+    if name == "c4":
+        return make_c4(n if n is not None else 1 << 21, seed if seed is not None else 4)
+    if name == "c5":
+        n = n if n is not None else 1 << 21
+        arena, offs, lens = make_docs(n, seed if seed is not None else 5, 4032, 4160, maker=_make_doc_c5)
+        cfg = c5_auth_config()
+        return Workload("c5", arena, offs, lens, cfg.authorization[0].rules,
+                        f"{n} docs of 4096+-64 B x full authz phase (4 when, 4 authz x (2 when + 16 rules), "
+                        "4 response selectors)", auth_config=cfg)
     raise ValueError(f"unknown workload {name!r}")

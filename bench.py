@@ -1,6 +1,6 @@
 """bench.py — headline benchmark (BASELINE.json metric) for the pattern-matching hot path.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3] [--n N_REQUESTS]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4] [--n N_REQUESTS]
 
 A step = one pass of the hot path (ajx kernels behind authjx_eval_batch_device) over one
 batch of N synthetic Authorization-JSON documents already resident in HBM. N=1 runs the
@@ -8,7 +8,8 @@ config BASELINE.json's metric is quoted on that fits one GPU (configs[1], "c2": 
 requests x 16 eq/neq/incl patterns). Multi-GPU: one process per GPU
 (torch.distributed.run), each rank evaluates its own shard (weak scaling, no data-path
 collective); the timed region is bracketed by barrier + synchronize, the max over ranks
-is reported. Rank 0 prints one JSON line.
+is reported. Rank 0 prints one JSON line. c4 (multi-tenant: 10k AuthConfigs, per-request
+set ids from the host index) defaults to 2M requests per GPU (16M over 8 GPUs).
 """
 import argparse
 import json
@@ -31,14 +32,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2")
-    ap.add_argument("--n", type=int, default=1 << 20, help="requests per GPU per step")
+    ap.add_argument("--n", type=int, default=None, help="requests per GPU per step (c2/c3 1M, c4 2M)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
 
-def cpu_baseline(w, n_patterns, target_s, gpu_tri, gpu_bm):
+def cpu_baseline(w, rpr, target_s, gpu_tri, gpu_bm):
     """Oracle (C restatement, oracle/) on a bounded sample of the same workload; also the
     parity check of the GPU results on that sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -46,11 +47,16 @@ def cpu_baseline(w, n_patterns, target_s, gpu_tri, gpu_bm):
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     threads = max(1, min(threads, 16))
-    pats, nodes, root = w.expr.flatten()
-    rs = pyoracle.Ruleset([(p.selector, int(p.operator), p.value) for p in pats], nodes, root)
+    rss = [pyoracle.Ruleset.from_expression(e) for e in w.sets]
+    sor = w.set_of_req
     pilot = min(w.n, 16384)
+
+    def run(k):
+        return pyoracle.eval_batch(rss, w.arena, w.offs[:k], w.lens[:k], nthreads=threads,
+                                   set_of_req=None if sor is None else sor[:k])
+
     t0 = time.perf_counter()
-    pyoracle.eval_batch([rs], w.arena, w.offs[:pilot], w.lens[:pilot], nthreads=threads)
+    run(pilot)
     dt = max(time.perf_counter() - t0, 1e-6)
     # the whole batch when it fits the time budget (repeated passes up to ~target_s), else
     # a prefix of it
@@ -58,11 +64,11 @@ def cpu_baseline(w, n_patterns, target_s, gpu_tri, gpu_bm):
     reps = max(1, int(target_s / (dt * sample / pilot)))
     t0 = time.perf_counter()
     for _ in range(reps):
-        tri, err, bm = pyoracle.eval_batch([rs], w.arena, w.offs[:sample], w.lens[:sample], nthreads=threads)
+        tri, err, bm = run(sample)
     dt = time.perf_counter() - t0
-    mism = int((tri != gpu_tri[:sample]).sum()) + int((bm != gpu_bm[:sample]).any(axis=1).sum())
+    mism = int((tri != gpu_tri[:sample]).sum()) + int((bm != gpu_bm[:sample, :bm.shape[1]]).any(axis=1).sum())
     return {
-        "value": reps * sample * n_patterns / dt,
+        "value": reps * int(rpr[:sample].sum()) / dt,
         "unit": "request×rule evals/s",
         "decisions_per_s": reps * sample / dt,
         "cores": threads,
@@ -129,13 +135,15 @@ def main():
     from authorino_amd import runtime, workloads
 
     w = workloads.make(args.workload, n=args.n, seed=1000 + rank)
-    R = w.n_patterns
+    rpr = w.patterns_per_request()  # R of each request's rule set
+    R = int(max(len(e.flatten()[0]) for e in w.sets))
     ctx = runtime.Context(local)
-    rs = ctx.compile_expression(w.expr)
+    rss = [ctx.compile_expression(e) for e in w.sets]
 
     arena = torch.from_numpy(w.arena).to(dev)
     offs = torch.from_numpy(w.offs.view(np.int64)).to(dev)
     lens = torch.from_numpy(w.lens.view(np.int32)).to(dev)
+    sor = torch.from_numpy(w.set_of_req.view(np.int32)).to(dev) if w.set_of_req is not None else None
     words = (R + 63) // 64
     tri = torch.empty(w.n, dtype=torch.uint8, device=dev)
     err = torch.empty(w.n, dtype=torch.int32, device=dev)
@@ -146,13 +154,13 @@ def main():
     sp = stream.cuda_stream
 
     def step():
-        ctx.eval_device([rs], arena, offs, lens, tri, err, bm, stream=sp)
+        ctx.eval_device(rss, arena, offs, lens, tri, err, bm, set_of_req=sor, stream=sp)
 
     elapsed, kern_ms = timed_steps(step, args.steps, args.warmup, dist, torch, dev, stream)
 
     total_req = w.n * args.steps * world
-    value = total_req * R / elapsed
-    algo_bytes = int(w.lens.astype(np.int64).sum()) + w.n * (math.ceil(R / 8) + 1)
+    value = int(rpr.sum()) * args.steps * world / elapsed  # shards are equal-sized (weak scaling)
+    algo_bytes = int(w.lens.astype(np.int64).sum()) + int(((rpr + 7) // 8 + 1).sum())
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     try:
@@ -165,7 +173,7 @@ def main():
 
     cpu, parity = None, None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu, parity = cpu_baseline(w, R, args.cpu_seconds, tri.cpu().numpy(), bm.cpu().numpy().view(np.uint64))
+        cpu, parity = cpu_baseline(w, rpr, args.cpu_seconds, tri.cpu().numpy(), bm.cpu().numpy().view(np.uint64))
     undecided = int((tri == runtime.UNDECIDED).sum().item())
     exact_path = ctx.last_exact_count()  # requests the single-pass kernel handed to the exact scan
 
@@ -188,8 +196,9 @@ def main():
                 "workload": args.workload,
                 "description": w.description,
                 "requests_per_gpu": w.n,
-                "patterns": R,
-                "selectors": rs.n_selectors,
+                "patterns": R if w.set_of_req is None else float(rpr.mean()),
+                "selectors": rss[0].n_selectors if len(rss) == 1 else float(np.mean([r.n_selectors for r in rss])),
+                "auth_configs": len(rss),
                 "doc_bytes_mean": float(w.lens.mean()),
                 "parallelism": f"dp{world} (independent request shards, no collective)",
             },

@@ -23,6 +23,13 @@
  *                           micro-batch of Authorization-JSON documents; its callers are
  *                           pkg/evaluators/authorization/json.go:19 (JSON rules) and
  *                           pkg/service/auth_pipeline.go:382 (every `when` gate).
+ *   authjx_select_batch[_device]
+ *                           pkg/json/json.go:41-53 JSONValue.ResolveFor's
+ *                           gjson.Get(authJSON, pattern) (and the per-placeholder Get of
+ *                           ReplaceJSONPlaceholders, :96-151) for a micro-batch: the
+ *                           selector values behind response headers
+ *                           (pkg/evaluators/response.go:150-174), returned as spans of
+ *                           the document that the host formats (Value()/String()).
  *   authjx_pattern_error    the static error a pattern yields (regexp.Compile's
  *                           "error parsing regexp: ..." or expressions.go:94
  *                           "unsupported operator for json authorization").
@@ -140,6 +147,40 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
                       const uint64_t* offs, const uint32_t* lens, uint32_t n,
                       uint8_t* out_tristate, int32_t* out_err_idx, uint64_t* out_bitmap,
                       uint32_t bitmap_stride_words);
+
+/* gjson.Get(doc, selector) as a span of the document. type is gjson.Type
+ * (AUTHJX_JSON_*); start is relative to the document; for strings the span includes the
+ * quotes and esc = 1 when the contents hold a backslash escape. A missing path is
+ * {0, 0, AUTHJX_JSON_NULL}. AUTHJX_JSON_UNSUPPORTED: the selector uses gjson syntax the
+ * device does not compile (its pattern_status is AUTHJX_PAT_UNSUPPORTED). */
+#define AUTHJX_JSON_NULL 0
+#define AUTHJX_JSON_FALSE 1
+#define AUTHJX_JSON_NUMBER 2
+#define AUTHJX_JSON_STRING 3
+#define AUTHJX_JSON_TRUE 4
+#define AUTHJX_JSON_JSON 5
+#define AUTHJX_JSON_UNSUPPORTED 255
+typedef struct {
+    uint32_t start;
+    uint32_t len;
+    uint8_t type;
+    uint8_t esc;
+    uint16_t reserved;
+} authjx_value;
+
+/* Resolve the selector of every pattern of `sets[set_of_req[r]]` (operators and values
+ * are ignored; compile the selectors as a tree of AUTHJX_OP_EQ patterns with root -1)
+ * for every request: d_out_values[r * values_stride + p], values_stride >= the largest
+ * n_patterns. Device buffers, asynchronous on `stream` (NULL = the context's stream). */
+int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                               const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
+                               const uint32_t* d_lens, uint32_t n, authjx_value* d_out_values,
+                               uint32_t values_stride, void* stream);
+/* Same from host buffers; synchronous. */
+int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                        const uint32_t* set_of_req, const uint8_t* arena, uint64_t arena_len,
+                        const uint64_t* offs, const uint32_t* lens, uint32_t n, authjx_value* out_values,
+                        uint32_t values_stride);
 
 /* Route every request through the exact per-selector scan kernel instead of the
  * single-pass kernel (results are identical; used to cross-check the two paths). */

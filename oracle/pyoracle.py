@@ -119,6 +119,21 @@ def gjson_get(doc, path) -> Tuple[int, bytes, bytes]:
     return out
 
 
+def gjson_span(doc, path) -> Tuple[int, int, int]:
+    """-> (type, start, length): gjson.Get's Raw as a span of the document"""
+    L = lib()
+    d, p = _b(doc), _b(path)
+    buf = C.create_string_buffer(d, len(d))
+    r = _Result()
+    rc = L.or_gjson_get(buf, len(d), p, len(p), C.byref(r))
+    if rc != 0:
+        raise ValueError(f"oracle: unsupported selector {path!r}")
+    start = (r.raw - C.addressof(buf)) if r.raw_len else 0
+    out = (r.type, start, r.raw_len)
+    L.or_result_free(C.byref(r))
+    return out
+
+
 def gjson_array(doc, path) -> List[bytes]:
     L = lib()
     d, p = _b(doc), _b(path)

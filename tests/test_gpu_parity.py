@@ -277,3 +277,77 @@ def test_pipeline_batch_on_device():
     for g, w in zip(got, want):
         assert (g.code, g.message, g.skipped, g.denied_by, g.authorization) == \
                (w.code, w.message, w.skipped, w.denied_by, w.authorization)
+
+
+def test_multi_tenant_c4(ctx):
+    """C4: 10k AuthConfigs compiled to device tables, per-request set ids from the host
+    index, one batch bucketed by AuthConfig, against the oracle on the same selection."""
+    from authorino_amd import workloads
+
+    w = workloads.make("c4", n=60000, seed=41)
+    sets = [ctx.compile_expression(e) for e in w.exprs]
+    assert all(st == 0 for s in sets for st in s.status)
+    tri, err, bm = ctx.eval_host_arena(sets, w.arena, w.offs, w.lens, set_of_req=w.set_of_req)
+    osets = [O.Ruleset.from_expression(e) for e in w.exprs]
+    otri, oerr, obm = _oracle(None, w.arena, w.offs, w.lens, set_of_req=w.set_of_req, sets=osets)
+    assert (tri == 3).sum() == 0
+    assert np.array_equal(tri, otri)
+    assert np.array_equal(err, oerr)
+    assert np.array_equal(bm, obm)
+    assert 0 < (tri == 1).sum() < w.n
+
+
+def test_select_values_match_oracle(ctx):
+    """authjx_select_batch (gjson.Get spans for response selectors)
+    against the oracle's Get on random documents (escapes, numbers, containers, missing
+    paths), on the reference's json_test.go document and on C5 documents."""
+    from authorino_amd import workloads
+    from test_response_host import DOC, _rand_doc
+
+    rng = np.random.default_rng(12)
+    docs, paths = [DOC], ["auth.identity.username", "auth.identity.address", "auth.identity.roles",
+                          "auth.identity.exp", r"auth.identity.github\.com", "auth.identity.email_verified", "nope"]
+    cases = [(DOC, p) for p in paths]
+    for _ in range(400):
+        d, ps = _rand_doc(rng)
+        cases += [(d, p) for p in ps]
+    w = workloads.make("c5", n=256, seed=52)
+    sel5 = ["auth.identity.sub", "auth.identity.exp", "auth.identity.realm_access.roles", "auth.metadata.tenant",
+            "auth.identity.resource_access.talker-api.roles", "context.request.http.host", "auth.identity.acr"]
+    cases += [(w.doc(i), p) for i in range(w.n) for p in sel5]
+    # one selector ruleset per distinct path; one request per (doc, path)
+    uniq = sorted({p for _, p in cases})
+    sets = {p: ctx.compile([(p, 1, "")], [], -1) for p in uniq}
+    order = [sets[p] for p in uniq]
+    sid = {p: i for i, p in enumerate(uniq)}
+    sor = np.array([sid[p] for _, p in cases], dtype=np.uint32)
+    blobs = [d for d, _ in cases]
+    lens = np.array([len(b) for b in blobs], dtype=np.uint32)
+    offs = np.zeros(len(blobs), dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1])
+    arena = np.frombuffer(b"".join(blobs), dtype=np.uint8)
+    got = ctx.select_host_arena(order, arena, offs, lens, set_of_req=sor)
+    for k, (d, p) in enumerate(cases):
+        t, st, ln = O.gjson_span(d, p)
+        g = got[k, 0]
+        assert (int(g[2]) & 0xFF, int(g[0]), int(g[1])) == (t, st, ln), (d[:200], p)
+
+
+def test_c5_full_phase_on_device(ctx):
+    """C5: `when` gates + 4 authz configs + response headers on the device against the
+    same phase through the oracle (headers compared byte for byte)."""
+    from test_pipeline_host import OracleCtx
+
+    from authorino_amd import pipeline as P
+    from authorino_amd import workloads
+
+    w = workloads.make("c5", n=3000, seed=53)
+    docs = [w.doc(i) for i in range(w.n)]
+    got = P.AuthPipelineBatch(w.auth_config, ctx=ctx).evaluate(docs)
+    want = P.AuthPipelineBatch(w.auth_config, ctx=OracleCtx()).evaluate(docs)
+    n_ok = 0
+    for g, o in zip(got, want):
+        assert (g.code, g.message, g.skipped, g.denied_by, g.authorization, g.headers, g.metadata) == \
+               (o.code, o.message, o.skipped, o.denied_by, o.authorization, o.headers, o.metadata)
+        n_ok += bool(g.headers)
+    assert 0 < n_ok < w.n

@@ -85,3 +85,25 @@ def test_port_retry_and_batch_selection():
     assert ix.lookup(c, "api.r0.example.com:443") == 2
     sel = ix.select_sets(c, ["t1.example.com", "x.r0.example.com", "nope.example.net", "t1.example.com:1"])
     assert sel.dtype == np.int64 and sel.tolist() == [0, 2, -1, 0]
+
+
+def test_c4_workload_selection_and_bucketing():
+    """The C4 batch: every request's set id is what the index lookup (with the :port
+    retry) gives for its host, unknown hosts are dropped, and the batch is bucketed."""
+    from authorino_amd import workloads as W
+
+    idx, exprs = W.c4_index_and_rules(600, 20, seed=4)
+    rng = np.random.default_rng(5)
+    hosts = W.c4_hosts(3000, 600, 20, rng)
+    sel = ix.select_sets(idx, hosts)
+    for h, s in zip(hosts, sel):
+        if h.startswith("u"):
+            assert s == -1
+        elif h.startswith("h"):
+            assert exprs[s] is exprs[580 + int(h.split(".")[1][1:])]
+        else:
+            assert s == int(h.split(".")[0][1:])
+    w = W.make_c4(2000, seed=9, n_configs=600, n_wild=20)
+    assert w.n == 2000 and np.all(np.diff(w.set_of_req.astype(np.int64)) >= 0)
+    assert all(8 <= len(e.flatten()[0]) <= 32 for e in w.exprs)
+    assert sum(any(p.operator == 5 for p in e.flatten()[0]) for e in w.exprs) > 20

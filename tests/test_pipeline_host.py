@@ -28,14 +28,34 @@ class _OracleRuleset:
         return self.rs.error(i)
 
 
+class _OracleSelectors:
+    def __init__(self, pats):
+        self.paths = [p[0] for p in pats]
+        self.n_patterns = len(pats)
+        self.status = [0] * len(pats)
+
+
 class OracleCtx:
-    """Stand-in for runtime.Context with the same two calls the pipeline makes."""
+    """Stand-in for runtime.Context with the calls the pipeline makes."""
 
     def __init__(self):
         self.launches = 0
 
     def compile_expression(self, expr):
         return _OracleRuleset(expr)
+
+    def compile(self, pats, nodes, root):  # selector-only rulesets (response selectors)
+        return _OracleSelectors(pats)
+
+    def select_host_arena(self, sets, arena, offs, lens, set_of_req=None):
+        n = len(lens)
+        out = np.zeros((n, max(s.n_patterns for s in sets), 3), dtype=np.uint32)
+        for r in range(n):
+            doc = arena[int(offs[r]):int(offs[r]) + int(lens[r])].tobytes()
+            for p, path in enumerate(sets[0 if set_of_req is None else int(set_of_req[r])].paths):
+                t, st, ln = O.gjson_span(doc, path)
+                out[r, p] = (st, ln, t)
+        return out
 
     def eval_host_arena(self, sets, arena, offs, lens, set_of_req=None, with_bitmap=True):
         self.launches += 1
