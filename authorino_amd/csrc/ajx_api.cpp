@@ -37,6 +37,9 @@ struct authjx_ctx {
     uint32_t slow_cap = 0;
     uint64_t* d_rows = nullptr;  // stage-A capture rows
     size_t rows_cap = 0;         // in u64
+    uint32_t* d_perm = nullptr;  // length-bucketed request order (+ 2 x 1024 u32 histogram)
+    uint32_t perm_cap = 0;
+    int len_sort = 1;            // order requests by length class before the single-pass kernel
     int force_scan = 0;
     int ablate = 0;  // profiling only: run a reduced stage A (1 loads, 2 loads+classify)
     float last_ms = 0.f;
@@ -113,6 +116,7 @@ void authjx_shutdown(authjx_ctx* ctx) {
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_slow) (void)hipFree(ctx->d_slow);
     if (ctx->d_rows) (void)hipFree(ctx->d_rows);
+    if (ctx->d_perm) (void)hipFree(ctx->d_perm);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -187,7 +191,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     HIP_OK(hipSetDevice(ctx->device));
     int rc = ensure_sets(ctx, sets, n_sets, s);
     if (rc != AUTHJX_OK) return rc;
-    if (!ctx->force_scan && (n > ctx->slow_cap || (size_t)n * row_stride > ctx->rows_cap)) {
+    if (!ctx->force_scan && (n > ctx->slow_cap || n > ctx->perm_cap || (size_t)n * row_stride > ctx->rows_cap)) {
         // growing the work buffers: no batch in flight on this context may still use them
         HIP_OK(hipStreamSynchronize(s));
         if (n > ctx->slow_cap) {
@@ -196,6 +200,13 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
             ctx->slow_cap = 0;
             HIP_OK(hipMalloc(&ctx->d_slow, ((size_t)n + 1) * sizeof(uint32_t)));
             ctx->slow_cap = n;
+        }
+        if (n > ctx->perm_cap) {
+            if (ctx->d_perm) (void)hipFree(ctx->d_perm);
+            ctx->d_perm = nullptr;
+            ctx->perm_cap = 0;
+            HIP_OK(hipMalloc(&ctx->d_perm, ((size_t)n + 2048) * sizeof(uint32_t)));
+            ctx->perm_cap = n;
         }
         if ((size_t)n * row_stride > ctx->rows_cap) {
             if (ctx->d_rows) (void)hipFree(ctx->d_rows);
@@ -209,12 +220,20 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     if (ctx->force_scan)
         HIP_OK(ajx::launch_eval_scan(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
-    else
+    else {
+        // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
+        // caller's bucketing by AuthConfig), the default kernel, batches worth sorting
+        const uint32_t* perm = nullptr;
+        if (ctx->len_sort && n_sets == 1 && ctx->ablate == 0 && n >= 4096) {
+            HIP_OK(ajx::launch_len_order(d_lens, n, ctx->d_perm + n, ctx->d_perm, s));
+            perm = ctx->d_perm;
+        }
         HIP_OK(ajx::launch_eval_fast(
             ctx->d_sets, d_set_of_req,
             (n_sets == 1 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes) ? (uint32_t)sets[0]->c.blob.size() : 0u,
             d_arena, d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words, ctx->d_rows,
-            row_stride, ctx->d_slow, ctx->d_slow + 1, s, ctx->ablate));
+            row_stride, ctx->d_slow, ctx->d_slow + 1, s, ctx->ablate, perm));
+    }
     HIP_OK(hipEventRecord(ctx->ev1, s));
     return AUTHJX_OK;
 }
@@ -291,6 +310,14 @@ int authjx_debug_ablate(authjx_ctx* ctx, int mode) {
     if (!ctx) return AUTHJX_EINVAL;
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->ablate = mode;
+    return AUTHJX_OK;
+}
+
+// Profiling only (not in authjx.h): turn the length-bucketed request order off / on.
+int authjx_debug_len_sort(authjx_ctx* ctx, int on) {
+    if (!ctx) return AUTHJX_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->len_sort = on ? 1 : 0;
     return AUTHJX_OK;
 }
 

@@ -32,6 +32,11 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode = 0);
+                            int mode = 0, const uint32_t* d_perm = nullptr);
+
+// Length-bucketed request order for the single-pass kernel: d_perm[n] = request ids,
+// longest 32-byte length class first; d_hist needs 2 * 1024 u32 of scratch.
+hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist, uint32_t* d_perm,
+                            hipStream_t stream);
 
 }  // namespace ajx

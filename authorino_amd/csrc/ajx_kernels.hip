@@ -237,10 +237,13 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused(con
                                                       uint32_t* __restrict__ slow_count,
                                                       uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
                                                       int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
-                                                      uint32_t stride, uint32_t ring_off) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)]);
-    if (r >= n) return;
+                                                      uint32_t stride, uint32_t ring_off,
+                                                      const uint32_t* __restrict__ perm) {
+    // work-item k takes request perm[k] (length-bucketed order, see ajx_len_scatter) or k
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t r = k < n ? (perm ? perm[k] : k) : 0u;
+    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : set_of_req[r]]);
+    if (k >= n) return;
     uint64_t* row = rows + (size_t)r * row_stride;
     const uint8_t* d = arena + offs[r];
     if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off))) {
@@ -356,6 +359,82 @@ __global__ __launch_bounds__(kLinesBlock, AJX_LINES_WAVES) void ajx_scan_lines(
     if (out_err) out_err[r] = ep;
 }
 
+// ---------------------------------------------------------------------------------
+// Length bucketing: a wave of the single-pass kernel runs each window's token loop as
+// long as its busiest lane, and the whole document loop as long as its longest
+// document, so the 64 requests of a wave should have similar lengths. A counting sort
+// by 32-byte length class (longest first) gives the order work-items take requests in;
+// outputs still go to each request's own index. Three small launches over lens[] (4 B
+// per request each).
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kLenBuckets = 1024;
+
+__device__ __forceinline__ uint32_t len_bucket(uint32_t len) {
+    const uint32_t b = len >> 5;
+    return kLenBuckets - 1u - (b < kLenBuckets ? b : kLenBuckets - 1u);
+}
+
+__global__ __launch_bounds__(kLenBuckets) void ajx_len_hist(const uint32_t* __restrict__ lens, uint32_t n,
+                                                            uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kLenBuckets];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        atomicAdd(&h[len_bucket(lens[i])], 1u);
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+// exclusive scan of the histogram into per-class cursors (one workgroup)
+__global__ __launch_bounds__(kLenBuckets) void ajx_len_scan(const uint32_t* __restrict__ hist,
+                                                            uint32_t* __restrict__ cursor) {
+    __shared__ uint32_t s[kLenBuckets];
+    const uint32_t t = threadIdx.x;
+    const uint32_t own = hist[t];
+    s[t] = own;
+    __syncthreads();
+    for (uint32_t o = 1; o < kLenBuckets; o <<= 1) {
+        const uint32_t v = t >= o ? s[t - o] : 0u;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    cursor[t] = s[t] - own;
+}
+
+// perm[cursor[class] + rank] = request; one global atomic per (workgroup, class)
+__global__ __launch_bounds__(kLenBuckets) void ajx_len_scatter(const uint32_t* __restrict__ lens, uint32_t n,
+                                                               uint32_t* __restrict__ cursor,
+                                                               uint32_t* __restrict__ perm) {
+    __shared__ uint32_t cnt[kLenBuckets];
+    __shared__ uint32_t base[kLenBuckets];
+    cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t b = 0, rank = 0;
+    if (i < n) {
+        b = len_bucket(lens[i]);
+        rank = atomicAdd(&cnt[b], 1u);
+    }
+    __syncthreads();
+    if (cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
+    __syncthreads();
+    if (i < n) perm[base[b] + rank] = i;
+}
+
+hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist, uint32_t* d_perm,
+                            hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(d_hist, 0, 2 * kLenBuckets * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const uint32_t blocks = (n + kLenBuckets - 1) / kLenBuckets;
+    hipLaunchKernelGGL(ajx_len_hist, dim3(blocks < 512 ? blocks : 512), dim3(kLenBuckets), 0, stream, d_lens, n,
+                       d_hist);
+    hipLaunchKernelGGL(ajx_len_scan, dim3(1), dim3(kLenBuckets), 0, stream, d_hist, d_hist + kLenBuckets);
+    hipLaunchKernelGGL(ajx_len_scatter, dim3(blocks), dim3(kLenBuckets), 0, stream, d_lens, n, d_hist + kLenBuckets,
+                       d_perm);
+    return hipGetLastError();
+}
+
 // gjson.Get per pattern selector (the response / header selectors of SURVEY.md §8 a14):
 // one work-item per request, the exact device Get (gj_get) for each of the ruleset's
 // patterns; out[r * stride + p] = {start (relative to the document), len, type, esc}.
@@ -419,7 +498,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode) {
+                            int mode, const uint32_t* d_perm) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
     // small blobs: 4-wave groups (measured faster on c2); larger ones share one copy per
@@ -494,11 +573,11 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     } else if (shared) {  // mode 0 (default): the single-pass kernel
         hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
                            d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                           stride, ring_off);
+                           stride, ring_off, d_perm);
     } else {
         hipLaunchKernelGGL((ajx_scan_fused<false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
                            d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                           stride, ring_off);
+                           stride, ring_off, d_perm);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;

@@ -1,7 +1,8 @@
 """Profiling helper: time the fast-path variants interleaved in one process
 (cdna_hip_programming.md §5.4 rule 24) and print one JSON line. Modes (authjx_debug_ablate):
 0 single-pass kernel (default), 5 line engine, 11 line engine loads + ring writes only,
-12 + classification, 1/2 single-pass loads / + classification, 3 stage A / stage B split."""
+12 + classification, 1/2 single-pass loads / + classification, 3 stage A / stage B split;
+100 + m: mode m without the length-bucketed request order."""
 import ctypes as C
 import json
 import os
@@ -22,6 +23,7 @@ ctx = runtime.Context(0)
 rs = ctx.compile_expression(w.expr)
 L = runtime.load_library()
 L.authjx_debug_ablate.argtypes = [C.c_void_p, C.c_int]
+L.authjx_debug_len_sort.argtypes = [C.c_void_p, C.c_int]
 arena = torch.from_numpy(w.arena).to(dev)
 offs = torch.from_numpy(w.offs.view(np.int64)).to(dev)
 lens = torch.from_numpy(w.lens.view(np.int32)).to(dev)
@@ -36,7 +38,8 @@ res = {m: [] for m in MODES}
 outs = {}
 for rep in range(6):
     for mode in MODES:
-        L.authjx_debug_ablate(ctx._h, mode)
+        L.authjx_debug_ablate(ctx._h, mode % 100)
+        L.authjx_debug_len_sort(ctx._h, 0 if mode >= 100 else 1)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         ctx.eval_device([rs], arena, offs, lens, tri, err, bm, stream=stream.cuda_stream)
