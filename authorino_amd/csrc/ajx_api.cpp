@@ -224,7 +224,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
         // caller's bucketing by AuthConfig), the default kernel, batches worth sorting
         const uint32_t* perm = nullptr;
-        if (ctx->len_sort && n_sets == 1 && ctx->ablate == 0 && n >= 4096) {
+        if (ctx->len_sort && (n_sets == 1 || ctx->len_sort > 1) && ctx->ablate == 0 && n >= 4096) {
             HIP_OK(ajx::launch_len_order(d_lens, n, ctx->d_perm + n, ctx->d_perm, s));
             perm = ctx->d_perm;
         }
@@ -313,11 +313,12 @@ int authjx_debug_ablate(authjx_ctx* ctx, int mode) {
     return AUTHJX_OK;
 }
 
-// Profiling only (not in authjx.h): turn the length-bucketed request order off / on.
+// Profiling only (not in authjx.h): the length-bucketed request order off (0), for
+// single-ruleset batches (1, default) or for every batch (2).
 int authjx_debug_len_sort(authjx_ctx* ctx, int on) {
     if (!ctx) return AUTHJX_EINVAL;
     std::lock_guard<std::mutex> lock(ctx->mu);
-    ctx->len_sort = on ? 1 : 0;
+    ctx->len_sort = on;  // 0 off, 1 single-ruleset batches, 2 also multi-tenant batches
     return AUTHJX_OK;
 }
 

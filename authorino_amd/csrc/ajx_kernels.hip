@@ -363,14 +363,15 @@ __global__ __launch_bounds__(kLinesBlock, AJX_LINES_WAVES) void ajx_scan_lines(
 // Length bucketing: a wave of the single-pass kernel runs each window's token loop as
 // long as its busiest lane, and the whole document loop as long as its longest
 // document, so the 64 requests of a wave should have similar lengths. A counting sort
-// by 32-byte length class (longest first) gives the order work-items take requests in;
-// outputs still go to each request's own index. Three small launches over lens[] (4 B
+// by 8-byte length class (longest first; documents over 8 KiB share the last class)
+// gives the order work-items take requests in; outputs still go to each request's own
+// index. Three small launches over lens[] (4 B
 // per request each).
 // ---------------------------------------------------------------------------------
 constexpr uint32_t kLenBuckets = 1024;
 
 __device__ __forceinline__ uint32_t len_bucket(uint32_t len) {
-    const uint32_t b = len >> 5;
+    const uint32_t b = len >> 3;
     return kLenBuckets - 1u - (b < kLenBuckets ? b : kLenBuckets - 1u);
 }
 
