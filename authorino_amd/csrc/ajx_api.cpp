@@ -123,6 +123,11 @@ void authjx_shutdown(authjx_ctx* ctx) {
     delete ctx;
 }
 
+namespace {
+int finish_compile(authjx_ctx* ctx, authjx_ruleset* rs, int rc, const std::string& err, authjx_ruleset** out,
+                   int32_t* pattern_status, char* errbuf, size_t errcap);
+}
+
 int authjx_compile(authjx_ctx* ctx, const authjx_tree* tree, authjx_ruleset** out, int32_t* pattern_status,
                    char* errbuf, size_t errcap) {
     if (!ctx || !tree || !out) return AUTHJX_EINVAL;
@@ -130,6 +135,24 @@ int authjx_compile(authjx_ctx* ctx, const authjx_tree* tree, authjx_ruleset** ou
     authjx_ruleset* rs = new authjx_ruleset();
     std::string err;
     int rc = ajx::compile_tree(tree, &rs->c, &err);
+    return finish_compile(ctx, rs, rc, err, out, pattern_status, errbuf, errcap);
+}
+
+int authjx_compile_forest(authjx_ctx* ctx, const authjx_tree* trees, uint32_t n_trees, authjx_ruleset** out,
+                          int32_t* pattern_status, char* errbuf, size_t errcap) {
+    if (!ctx || !trees || !n_trees || !out) return AUTHJX_EINVAL;
+    *out = nullptr;
+    authjx_ruleset* rs = new authjx_ruleset();
+    std::string err;
+    int rc = ajx::compile_forest(trees, n_trees, &rs->c, &err);
+    return finish_compile(ctx, rs, rc, err, out, pattern_status, errbuf, errcap);
+}
+
+uint32_t authjx_ruleset_trees(const authjx_ruleset* rs) { return rs ? rs->c.n_trees : 0; }
+
+namespace {
+int finish_compile(authjx_ctx* ctx, authjx_ruleset* rs, int rc, const std::string& err, authjx_ruleset** out,
+                   int32_t* pattern_status, char* errbuf, size_t errcap) {
     if (errbuf && errcap) std::snprintf(errbuf, errcap, "%s", err.c_str());
     if (rc != AUTHJX_OK) {
         delete rs;
@@ -148,6 +171,7 @@ int authjx_compile(authjx_ctx* ctx, const authjx_tree* tree, authjx_ruleset** ou
     *out = rs;
     return AUTHJX_OK;
 }
+}  // namespace
 
 void authjx_free(authjx_ruleset* rs) {
     if (!rs) return;
@@ -179,7 +203,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     if (n_sets == 1) d_set_of_req = nullptr;  // every request uses sets[0] (uniform-ruleset kernels)
     uint32_t need_words = 0, max_sel = 0;
     for (uint32_t i = 0; i < n_sets; i++) {
-        if (!sets[i]) return AUTHJX_EINVAL;
+        if (!sets[i] || sets[i]->c.n_trees != sets[0]->c.n_trees) return AUTHJX_EINVAL;
         uint32_t w = (sets[i]->c.n_patterns + 63) / 64;
         if (w > need_words) need_words = w;
         if (sets[i]->c.n_selectors > max_sel) max_sel = sets[i]->c.n_selectors;
@@ -356,13 +380,15 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
     for (uint32_t r = 0; r < n; r++)
         if (offs[r] + lens[r] > arena_len) return AUTHJX_EINVAL;
     const bool with_sor = set_of_req != nullptr;
+    if (!sets || n_sets == 0 || !sets[0]) return AUTHJX_EINVAL;
+    const size_t nt = sets[0]->c.n_trees;  // results per request
     size_t o_arena = 0;
     size_t o_offs = round_up(o_arena + arena_len, 256);
     size_t o_lens = round_up(o_offs + (size_t)n * 8, 256);
     size_t o_sor = round_up(o_lens + (size_t)n * 4, 256);
     size_t o_tri = round_up(o_sor + (with_sor ? (size_t)n * 4 : 0), 256);
-    size_t o_err = round_up(o_tri + (size_t)n, 256);
-    size_t o_bm = round_up(o_err + (size_t)n * 4, 256);
+    size_t o_err = round_up(o_tri + (size_t)n * nt, 256);
+    size_t o_bm = round_up(o_err + (size_t)n * nt * 4, 256);
     size_t total = round_up(o_bm + (out_bitmap ? (size_t)n * bitmap_stride_words * 8 : 0), 256);
     std::lock_guard<std::mutex> batch_lock(ctx->batch_mu);
     {
@@ -390,8 +416,8 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
     if (rc != AUTHJX_OK) return rc;
     std::lock_guard<std::mutex> lock(ctx->mu);
     hipStream_t s = ctx->stream;
-    HIP_OK(hipMemcpyAsync(out_tristate, b + o_tri, n, hipMemcpyDeviceToHost, s));
-    if (out_err_idx) HIP_OK(hipMemcpyAsync(out_err_idx, b + o_err, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(out_tristate, b + o_tri, (size_t)n * nt, hipMemcpyDeviceToHost, s));
+    if (out_err_idx) HIP_OK(hipMemcpyAsync(out_err_idx, b + o_err, (size_t)n * nt * 4, hipMemcpyDeviceToHost, s));
     if (out_bitmap)
         HIP_OK(hipMemcpyAsync(out_bitmap, b + o_bm, (size_t)n * bitmap_stride_words * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));

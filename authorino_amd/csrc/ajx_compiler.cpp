@@ -110,11 +110,53 @@ struct Builder {
 
 }  // namespace
 
+namespace {
+int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, bool forest, CompiledRuleset* out,
+                 std::string* err);
+}
+
 int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err) {
     if (!tree) return AUTHJX_EINVAL;
+    return compile_core(tree, {tree->root}, false, out, err);
+}
+
+// Several trees over the same documents as one ruleset: patterns and nodes concatenated
+// in tree order (selectors shared by the trees share one trie path), one fold program per
+// tree (RulesetHdr::pad1[0] = tree count, pad1[1] = offset of {code_begin, code_len}[]).
+int compile_forest(const authjx_tree* trees, uint32_t n_trees, CompiledRuleset* out, std::string* err) {
+    if (!trees || n_trees == 0) return AUTHJX_EINVAL;
+    std::vector<authjx_pattern> pats;
+    std::vector<authjx_node> nodes;
+    std::vector<int32_t> roots;
+    for (uint32_t k = 0; k < n_trees; k++) {
+        const authjx_tree& t = trees[k];
+        if ((t.n_patterns && !t.patterns) || (t.n_nodes && !t.nodes) || t.root >= (int32_t)t.n_nodes)
+            return AUTHJX_EINVAL;
+        const int32_t po = (int32_t)pats.size(), no = (int32_t)nodes.size();
+        pats.insert(pats.end(), t.patterns, t.patterns + t.n_patterns);
+        for (uint32_t i = 0; i < t.n_nodes; i++) {
+            authjx_node nd = t.nodes[i];
+            if (nd.left >= (int32_t)t.n_nodes || nd.right >= (int32_t)t.n_nodes) return AUTHJX_EINVAL;
+            if (nd.kind == AUTHJX_NODE_PATTERN && (nd.pattern < 0 || (uint32_t)nd.pattern >= t.n_patterns))
+                return AUTHJX_EINVAL;
+            if (nd.left >= 0) nd.left += no;
+            if (nd.right >= 0) nd.right += no;
+            if (nd.kind == AUTHJX_NODE_PATTERN) nd.pattern += po;
+            nodes.push_back(nd);
+        }
+        roots.push_back(t.root < 0 ? -1 : t.root + no);
+    }
+    authjx_tree all{pats.data(), (uint32_t)pats.size(), nodes.data(), (uint32_t)nodes.size(), -1};
+    return compile_core(&all, roots, true, out, err);
+}
+
+namespace {
+int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, bool forest, CompiledRuleset* out,
+                 std::string* err) {
     const uint32_t np = tree->n_patterns, nn = tree->n_nodes;
     if ((np && !tree->patterns) || (nn && !tree->nodes)) return AUTHJX_EINVAL;
-    if (tree->root >= (int32_t)nn) return AUTHJX_EINVAL;
+    for (int32_t rt : roots)
+        if (rt >= (int32_t)nn) return AUTHJX_EINVAL;
 
     // ---- normalise the And/Or tree into n-ary fold nodes ----
     std::vector<int> visiting(nn, 0);
@@ -156,7 +198,8 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
         }
         visiting[(size_t)idx] = 0;
     };
-    NormNode root = tree->root < 0 ? NormNode{3} : norm(tree->root);
+    std::vector<NormNode> normed;
+    for (int32_t rt : roots) normed.push_back(rt < 0 ? NormNode{3} : norm(rt));
     if (bad) {
         if (err) *err = "malformed expression tree";
         return AUTHJX_EINVAL;
@@ -176,7 +219,13 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
                 code.push_back(C_CLOSE << 24);
         }
     };
-    emit(root, 0);
+    std::vector<uint32_t> root_code;  // {begin, len} per tree
+    for (const NormNode& rn : normed) {
+        const uint32_t b0 = (uint32_t)code.size();
+        emit(rn, 0);
+        root_code.push_back(b0);
+        root_code.push_back((uint32_t)code.size() - b0);
+    }
     if (max_depth > kMaxDepth) {
         if (err) *err = "expression nests And/Or deeper than the device fold stack";
         return AUTHJX_ELIMIT;
@@ -400,6 +449,11 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
     b.append(comps.data(), comps.size() * sizeof(Component));
     hdr.off_code = (uint32_t)b.align16();
     b.append(code.data(), code.size() * sizeof(uint32_t));
+    if (forest) {
+        hdr.pad1[0] = (uint32_t)roots.size();
+        hdr.pad1[1] = (uint32_t)b.align16();
+        b.append(root_code.data(), root_code.size() * sizeof(uint32_t));
+    }
     hdr.off_literals = (uint32_t)b.align16();
     lits.append(16, '\0');  // dword reads past a literal's end stay inside the pool
     b.append(lits.data(), lits.size());
@@ -446,7 +500,9 @@ int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err
     out->n_patterns = np;
     out->n_selectors = (uint32_t)sels.size();
     out->max_depth = max_depth;
+    out->n_trees = (uint32_t)roots.size();
     return AUTHJX_OK;
 }
+}  // namespace
 
 }  // namespace ajx

@@ -19,6 +19,7 @@ struct CompiledRuleset {
     uint32_t n_patterns = 0;
     uint32_t n_selectors = 0;
     uint32_t max_depth = 0;
+    uint32_t n_trees = 1;                     // fold programs (results per request)
 };
 
 // Split a gjson path into device components. Returns false when the path uses gjson
@@ -31,5 +32,7 @@ bool split_selector(const std::string& path, std::vector<PathComponent>* out);
 
 // Returns AUTHJX_OK or an AUTHJX_E* code (malformed tree, nesting over kMaxDepth).
 int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err);
+// Several trees as one ruleset (one scan of a document evaluates all of them).
+int compile_forest(const authjx_tree* trees, uint32_t n_trees, CompiledRuleset* out, std::string* err);
 
 }  // namespace ajx

@@ -73,17 +73,23 @@ __device__ __forceinline__ void eval_scan_one(uint32_t r, const uint8_t* const* 
             row[w] = word;
         }
     }
-    int32_t ep;
-    uint8_t t;
-    if (cache_pat) {
-        if (!out_bm)
-            for (uint32_t p = 0; p < np; p++) res[p] = eval(p);
-        t = run_fold(code, h->n_code, [&](uint32_t p) { return res[p]; }, &ep);
-    } else {
-        t = run_fold(code, h->n_code, eval, &ep);
+    if (cache_pat && !out_bm)
+        for (uint32_t p = 0; p < np; p++) res[p] = eval(p);
+    // one fold program per tree (a forest ruleset writes n_trees results per request)
+    const uint32_t nt = h->pad1[0] ? h->pad1[0] : 1u;
+    const uint32_t* rc = h->pad1[0] ? reinterpret_cast<const uint32_t*>(blob + h->pad1[1]) : nullptr;
+    for (uint32_t k = 0; k < nt; k++) {
+        const uint32_t* c = rc ? code + rc[2 * k] : code;
+        const uint32_t len = rc ? rc[2 * k + 1] : h->n_code;
+        int32_t ep;
+        uint8_t t;
+        if (cache_pat)
+            t = run_fold(c, len, [&](uint32_t p) { return res[p]; }, &ep);
+        else
+            t = run_fold(c, len, eval, &ep);
+        out_tri[(size_t)r * nt + k] = t;
+        if (out_err) out_err[(size_t)r * nt + k] = ep;
     }
-    out_tri[r] = t;
-    if (out_err) out_err[r] = ep;
 }
 
 __global__ __launch_bounds__(256) void ajx_eval_scan(const uint8_t* const* __restrict__ sets,
@@ -168,6 +174,27 @@ __device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t*
     });
 }
 
+// the And/Or fold of every tree of the ruleset on the pattern bitmaps; a forest ruleset
+// (authjx_compile_forest) writes its n_trees results at r * n_trees + k
+__device__ __forceinline__ void fold_outputs(uint32_t r, const uint8_t* blob, const RulesetHdr* h, const uint64_t t[2],
+                                             const uint64_t u[2], const uint64_t se[2],
+                                             uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err) {
+    const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
+    const uint32_t nt = h->pad1[0];
+    if (nt == 0) {
+        int32_t ep;
+        out_tri[r] = run_fold_bits(code, h->n_code, t, u, se, &ep);
+        if (out_err) out_err[r] = ep;
+        return;
+    }
+    const uint32_t* rc = reinterpret_cast<const uint32_t*>(blob + h->pad1[1]);
+    for (uint32_t k = 0; k < nt; k++) {
+        int32_t ep;
+        out_tri[(size_t)r * nt + k] = run_fold_bits(code + rc[2 * k], rc[2 * k + 1], t, u, se, &ep);
+        if (out_err) out_err[(size_t)r * nt + k] = ep;
+    }
+}
+
 // stage B for request r on its capture row: patterns, T bitmap, And/Or fold, outputs
 __device__ __forceinline__ void finish_request(uint32_t r, const uint8_t* blob, const uint8_t* d, const uint64_t* row,
                                                uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
@@ -182,11 +209,7 @@ __device__ __forceinline__ void finish_request(uint32_t r, const uint8_t* blob, 
         for (uint32_t w = 2; w < stride; w++) orow[w] = 0ull;
     }
     const uint64_t se[2] = {h->static_error[0], h->static_error[1]};
-    int32_t ep;
-    const uint8_t tri =
-        run_fold_bits(reinterpret_cast<const uint32_t*>(blob + h->off_code), h->n_code, t, u, se, &ep);
-    out_tri[r] = tri;
-    if (out_err) out_err[r] = ep;
+    fold_outputs(r, blob, h, t, u, se, out_tri, out_err);
 }
 
 // Stage A alone (profiling split / ablations): structural scan -> capture rows.
@@ -353,10 +376,7 @@ __global__ __launch_bounds__(kLinesBlock, AJX_LINES_WAVES) void ajx_scan_lines(
         for (uint32_t w = 2; w < stride; w++) orow[w] = 0ull;
     }
     const uint64_t se[2] = {h->static_error[0], h->static_error[1]};
-    int32_t ep;
-    const uint8_t tri = run_fold_bits(reinterpret_cast<const uint32_t*>(blob + h->off_code), h->n_code, t, u, se, &ep);
-    out_tri[r] = tri;
-    if (out_err) out_err[r] = ep;
+    fold_outputs(r, blob, h, t, u, se, out_tri, out_err);
 }
 
 // ---------------------------------------------------------------------------------

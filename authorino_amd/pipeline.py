@@ -122,6 +122,19 @@ class AuthPipelineBatch:
         self.levels = [[c for c in auth_config.authorization if c.priority == p] for p in prios]
         self._needs_regen = any(_selects_authorization(e) for lvl in self.levels[1:] for c in lvl
                                 for e in (c.conditions, c.rules))
+        # one forest ruleset for every expression of the phase when no later priority reads
+        # what an earlier one granted: one document scan per request for all of them
+        self._forest = None
+        self._col: Dict[int, int] = {}
+        if not self._needs_regen and hasattr(self.ctx, "compile_forest"):
+            uniq = []
+            for e in exprs:
+                if e is not None and id(e) not in self._col:
+                    self._col[id(e)] = len(uniq)
+                    uniq.append(e)
+            if uniq:
+                self._forest = self.ctx.compile_forest(uniq)
+        self._all = None
         rprios = sorted({c.priority for c in auth_config.response})
         self.response_levels = [[c for c in auth_config.response if c.priority == p] for p in rprios]
         self.selectors = ResponseSelectors(auth_config.response, self.ctx) if auth_config.response else None
@@ -133,6 +146,17 @@ class AuthPipelineBatch:
     # one launch: expression k of `exprs` on every request in `reqs`
     def _eval(self, exprs: Sequence[jsonexp.Expression], reqs: np.ndarray, arena, offs, lens):
         from . import runtime
+
+        if self._forest is not None:
+            if self._all is None or self._all[0] is not arena:
+                tri, err, _ = self.ctx.eval_host_arena([self._forest], arena, offs, lens, with_bitmap=False)
+                tri = tri.reshape(len(lens), -1)
+                if (tri == runtime.UNDECIDED).any():
+                    raise runtime.AuthjxError("device could not decide a document (AUTHJX_UNDECIDED)")
+                self._all = (arena, tri, err.reshape(len(lens), -1))
+            _, tri, err = self._all
+            cols = [self._col[id(e)] for e in exprs]
+            return tri[reqs][:, cols].T, err[reqs][:, cols].T, [self._forest] * len(exprs)
 
         sets = [self._rs[id(e)] for e in exprs]
         k = len(exprs)
@@ -166,6 +190,7 @@ class AuthPipelineBatch:
             return np.frombuffer(b"".join(ds) + b"\0", dtype=np.uint8), offs, lens
 
         arena, offs, lens = pack(docs)
+        self._all = None
         live = np.arange(n)
         # AuthConfig-level `when` (auth_pipeline.go:454-457): not met -> OK, skipped
         top = self.config.conditions
@@ -212,10 +237,10 @@ class AuthPipelineBatch:
                             res.message = str(UnauthorizedError())
             live = live[~denied]
         if self.selectors is not None and len(live):
-            self._responses(results, docs, live)
+            self._responses(results, docs, live, arena, offs, lens)
         return results
 
-    def _responses(self, results, docs, live):
+    def _responses(self, results, docs, live, arena_all, offs_all, lens_all):
         """Phase 4 for the requests that passed authorization (auth_pipeline.go:490-494)."""
         from . import runtime
 
@@ -233,7 +258,7 @@ class AuthPipelineBatch:
             conds = [c.conditions for c in level if c.conditions is not None]
             met = {}
             if conds:
-                tri, _, _ = self._eval(conds, idx, arena, offs, lens)
+                tri, _, _ = self._eval(conds, live, arena_all, offs_all, lens_all)
                 met = {id(e): tri[j] == runtime.T for j, e in enumerate(conds)}
             for c in level:
                 ok = met[id(c.conditions)] if c.conditions is not None else None

@@ -48,7 +48,8 @@ EXPORTS = [
     "authjx_init", "authjx_shutdown", "authjx_device_count", "authjx_compile", "authjx_free",
     "authjx_ruleset_patterns", "authjx_ruleset_selectors", "authjx_pattern_error",
     "authjx_eval_batch_device", "authjx_eval_batch", "authjx_last_kernel_ms", "authjx_set_exact_scan",
-    "authjx_last_exact_count", "authjx_select_batch_device", "authjx_select_batch",
+    "authjx_last_exact_count", "authjx_select_batch_device", "authjx_select_batch", "authjx_compile_forest",
+    "authjx_ruleset_trees",
 ]
 
 
@@ -77,6 +78,11 @@ def load_library(path: str = LIB_PATH):
         L.authjx_compile.argtypes = [C.c_void_p, C.POINTER(_Tree), C.POINTER(C.c_void_p), C.POINTER(C.c_int32),
                                      C.c_char_p, C.c_size_t]
         L.authjx_compile.restype = C.c_int
+        L.authjx_compile_forest.argtypes = [C.c_void_p, C.POINTER(_Tree), C.c_uint32, C.POINTER(C.c_void_p),
+                                            C.POINTER(C.c_int32), C.c_char_p, C.c_size_t]
+        L.authjx_compile_forest.restype = C.c_int
+        L.authjx_ruleset_trees.argtypes = [C.c_void_p]
+        L.authjx_ruleset_trees.restype = C.c_uint32
         L.authjx_free.argtypes = [C.c_void_p]
         L.authjx_free.restype = None
         L.authjx_ruleset_patterns.argtypes = [C.c_void_p]
@@ -141,6 +147,18 @@ class Context:
         pats, nodes, root = expr.flatten()
         return Ruleset(self, [(p.selector, int(p.operator), p.value) for p in pats], nodes, root)
 
+    def compile_forest(self, exprs) -> "Ruleset":
+        """Several expressions (None = nil) as one ruleset (authjx_compile_forest): one
+        scan per document, one result per expression."""
+        trees = []
+        for e in exprs:
+            if e is None:
+                trees.append(([], [], -1))
+            else:
+                pats, nodes, root = e.flatten()
+                trees.append(([(p.selector, int(p.operator), p.value) for p in pats], nodes, root))
+        return Ruleset(self, None, None, None, forest=trees)
+
     def eval_device(self, sets: Sequence["Ruleset"], arena, offs, lens, out_tri, out_err=None, out_bm=None,
                     set_of_req=None, stream=None) -> None:
         """Evaluate a batch resident in HBM (torch tensors on this device). Asynchronous."""
@@ -185,11 +203,12 @@ class Context:
     def eval_host_arena(self, sets, arena, offs, lens, set_of_req=None, with_bitmap=True):
         n = int(lens.shape[0])
         words = max(1, max((s.n_patterns + 63) // 64 for s in sets))
+        nt = sets[0].n_trees
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint32)
-        tri = np.zeros(max(n, 1), dtype=np.uint8)
-        err = np.zeros(max(n, 1), dtype=np.int32)
+        tri = np.zeros(max(n, 1) * nt, dtype=np.uint8)
+        err = np.zeros(max(n, 1) * nt, dtype=np.int32)
         bm = np.zeros((max(n, 1), words), dtype=np.uint64) if with_bitmap else None
         sor = None
         if set_of_req is not None:
@@ -202,6 +221,8 @@ class Context:
             C.c_void_p(err.ctypes.data), C.c_void_p(bm.ctypes.data) if bm is not None else None,
             words if bm is not None else 0)
         _check(rc, "authjx_eval_batch")
+        if nt > 1:
+            return tri.reshape(-1, nt)[:n], err.reshape(-1, nt)[:n], (bm[:n] if bm is not None else None)
         return tri[:n], err[:n], (bm[:n] if bm is not None else None)
 
     def select_host_arena(self, sets, arena, offs, lens, set_of_req=None) -> np.ndarray:
@@ -241,29 +262,41 @@ class Context:
 class Ruleset:
     """A compiled jsonexp tree resident in HBM (authjx_compile / authjx_free)."""
 
-    def __init__(self, ctx: Context, patterns, nodes, root):
+    def __init__(self, ctx: Context, patterns, nodes, root, forest=None):
         L = load_library()
         self.ctx = ctx
-        self.n_patterns = len(patterns)
         keep = []
-        parr = (_Pattern * max(len(patterns), 1))()
-        for i, (sel, op, val) in enumerate(patterns):
-            sb, vb = _b(sel), _b(val)
-            keep += [sb, vb]
-            parr[i] = _Pattern(sb, len(sb), int(op), vb, len(vb))
-        narr = (_Node * max(len(nodes), 1))()
-        for i, nd in enumerate(nodes):
-            narr[i] = _Node(*nd)
-        tree = _Tree(parr, len(patterns), narr, len(nodes), root)
-        st = (C.c_int32 * max(len(patterns), 1))()
+
+        def tree_of(patterns, nodes, root):
+            parr = (_Pattern * max(len(patterns), 1))()
+            for i, (sel, op, val) in enumerate(patterns):
+                sb, vb = _b(sel), _b(val)
+                keep.extend([sb, vb])
+                parr[i] = _Pattern(sb, len(sb), int(op), vb, len(vb))
+            narr = (_Node * max(len(nodes), 1))()
+            for i, nd in enumerate(nodes):
+                narr[i] = _Node(*nd)
+            keep.extend([parr, narr])
+            return _Tree(parr, len(patterns), narr, len(nodes), root)
+
+        trees = forest if forest is not None else [(patterns, nodes, root)]
+        self.offsets = list(np.cumsum([0] + [len(t[0]) for t in trees])[:-1])  # first pattern of each tree
+        self.n_patterns = sum(len(t[0]) for t in trees)
+        st = (C.c_int32 * max(self.n_patterns, 1))()
         err = C.create_string_buffer(512)
         h = C.c_void_p()
-        rc = L.authjx_compile(ctx._h, C.byref(tree), C.byref(h), st, err, 512)
+        if forest is None:
+            tree = tree_of(patterns, nodes, root)
+            rc = L.authjx_compile(ctx._h, C.byref(tree), C.byref(h), st, err, 512)
+        else:
+            tarr = (_Tree * len(trees))(*[tree_of(*t) for t in trees])
+            rc = L.authjx_compile_forest(ctx._h, tarr, len(trees), C.byref(h), st, err, 512)
         if rc != 0:
             raise AuthjxError(f"authjx_compile failed ({rc}): {err.value.decode(errors='replace')}")
         self._h = h
-        self.status = list(st)[: len(patterns)]
+        self.status = list(st)[: self.n_patterns]
         self.n_selectors = int(L.authjx_ruleset_selectors(h))
+        self.n_trees = int(L.authjx_ruleset_trees(h))
 
     def pattern_error(self, i: int) -> str:
         buf = C.create_string_buffer(1024)

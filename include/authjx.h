@@ -15,6 +15,9 @@
  *                           (flattened, see authjx_tree) is compiled once into
  *                           device-resident tables (selector paths, literal pool,
  *                           fold bytecode, regex DFAs).
+ *   authjx_compile_forest   the same compile point for every expression of one
+ *                           AuthConfig's authorization phase at once (one document scan
+ *                           per request for all of them).
  *   authjx_free             pkg/auth/auth.go:30-33 AuthConfigCleaner.Clean (called from
  *                           pkg/evaluators/config.go:42-68 before re-translate/delete).
  *   authjx_eval_batch[_device]
@@ -119,6 +122,19 @@ int authjx_device_count(void);
  * depends on them. errbuf (may be NULL) receives a diagnostic. */
 int authjx_compile(authjx_ctx* ctx, const authjx_tree* tree, authjx_ruleset** out,
                    int32_t* pattern_status, char* errbuf, size_t errcap);
+/* Compile several trees that read the same documents into ONE ruleset, so that one
+ * scan of a document evaluates all of them (an authorization phase: the AuthConfig-level
+ * `when`, each evaluator's `when` and rules — pkg/service/auth_pipeline.go:120-125,
+ * :287-322, :454-457). Patterns are numbered across the trees in order (tree k's
+ * pattern i is pattern sum_{j<k} n_patterns_j + i; pattern_status has that many
+ * entries); selectors shared by several trees are scanned once. Evaluating it writes
+ * one result per tree: d_out_tristate[r * n_trees + k] and d_out_err_idx[r * n_trees + k]
+ * (the error index in the forest's numbering). Every ruleset of one batch must have the
+ * same tree count. */
+int authjx_compile_forest(authjx_ctx* ctx, const authjx_tree* trees, uint32_t n_trees, authjx_ruleset** out,
+                          int32_t* pattern_status, char* errbuf, size_t errcap);
+/* Results per request of the ruleset (1 for authjx_compile). */
+uint32_t authjx_ruleset_trees(const authjx_ruleset* rs);
 void authjx_free(authjx_ruleset* rs);
 uint32_t authjx_ruleset_patterns(const authjx_ruleset* rs);
 uint32_t authjx_ruleset_selectors(const authjx_ruleset* rs);
@@ -129,8 +145,10 @@ size_t authjx_pattern_error(const authjx_ruleset* rs, uint32_t i, char* buf, siz
  *   sets[n_sets]      rulesets; request r uses sets[set_of_req ? set_of_req[r] : 0]
  *   d_set_of_req      device u32[n] (entries < n_sets) or NULL; ignored when n_sets == 1
  *   d_arena           device bytes; document r = d_arena[d_offs[r] .. + d_lens[r])
- *   d_out_tristate    device u8[n]  (AUTHJX_F/T/E/UNDECIDED)
- *   d_out_err_idx     device i32[n] pattern whose error decided an E, else -1 (may be NULL)
+ *   d_out_tristate    device u8[n * n_trees]  (AUTHJX_F/T/E/UNDECIDED; n_trees = 1 unless
+ *                     the rulesets come from authjx_compile_forest)
+ *   d_out_err_idx     device i32[n * n_trees] pattern whose error decided an E, else -1
+ *                     (may be NULL)
  *   d_out_bitmap      device u64[n * bitmap_stride_words]: bit p = pattern p evaluated to T
  *                     (every pattern evaluated, no short-circuit), may be NULL
  *   stream            hipStream_t (NULL = the context's stream). Asynchronous. */

@@ -351,3 +351,35 @@ def test_c5_full_phase_on_device(ctx):
                (o.code, o.message, o.skipped, o.denied_by, o.authorization, o.headers, o.metadata)
         n_ok += bool(g.headers)
     assert 0 < n_ok < w.n
+
+
+def test_forest_matches_single_rulesets(ctx):
+    """authjx_compile_forest: every tree of the C5 phase (+ c2's rules and a tree with a
+    static regex error) in one ruleset, one scan per document; per-tree results, error
+    indices (forest numbering) and pattern bits equal the trees compiled one by one, which
+    the oracle pins."""
+    from authorino_amd import jsonexp as J
+    from authorino_amd import workloads
+
+    w = workloads.make("c5", n=20000, seed=54)
+    cfg = w.auth_config
+    exprs = [cfg.conditions] + [e for c in cfg.authorization for e in (c.conditions, c.rules)]
+    exprs += [workloads.c2_expression(), J.Any(J.Pattern("auth.identity.sub", J.EqualOperator, "user-0042"),
+                                               J.Pattern("context.request.http.path", J.RegexOperator, "(["))]
+    forest = ctx.compile_forest(exprs)
+    assert forest.n_trees == len(exprs)
+    ftri, ferr, fbm = ctx.eval_host_arena([forest], w.arena, w.offs, w.lens)
+    assert ftri.shape == (w.n, len(exprs))
+    bits = np.unpackbits(fbm.view(np.uint8), axis=1, bitorder="little")
+    for k, e in enumerate(exprs):
+        rs = ctx.compile_expression(e)
+        tri, err, bm = ctx.eval_host_arena([rs], w.arena, w.offs, w.lens)
+        off = forest.offsets[k]
+        assert np.array_equal(ftri[:, k], tri), k
+        assert np.array_equal(ferr[:, k], np.where(err >= 0, err + off, -1)), k
+        tb = np.unpackbits(bm.view(np.uint8), axis=1, bitorder="little")[:, :rs.n_patterns]
+        assert np.array_equal(bits[:, off:off + rs.n_patterns], tb), k
+        if k < 3 or k == len(exprs) - 1:
+            otri, oerr, _ = _oracle(e, w.arena, w.offs, w.lens)
+            assert np.array_equal(tri, otri) and np.array_equal(err, oerr), k
+    assert (ftri[:, -1] == 2).any()  # the static error decides some requests

@@ -28,6 +28,17 @@ class _OracleRuleset:
         return self.rs.error(i)
 
 
+class _OracleForest:
+    def __init__(self, exprs):
+        self.trees = [_OracleRuleset(e) for e in exprs]
+        self.offsets = list(np.cumsum([0] + [t.n_patterns for t in self.trees])[:-1])
+        self.n_trees = len(self.trees)
+
+    def pattern_error(self, i):
+        k = max(j for j, o in enumerate(self.offsets) if o <= i and self.trees[j].n_patterns > i - o)
+        return self.trees[k].pattern_error(i - self.offsets[k])
+
+
 class _OracleSelectors:
     def __init__(self, pats):
         self.paths = [p[0] for p in pats]
@@ -44,6 +55,9 @@ class OracleCtx:
     def compile_expression(self, expr):
         return _OracleRuleset(expr)
 
+    def compile_forest(self, exprs):
+        return _OracleForest(exprs)
+
     def compile(self, pats, nodes, root):  # selector-only rulesets (response selectors)
         return _OracleSelectors(pats)
 
@@ -59,6 +73,12 @@ class OracleCtx:
 
     def eval_host_arena(self, sets, arena, offs, lens, set_of_req=None, with_bitmap=True):
         self.launches += 1
+        if isinstance(sets[0], _OracleForest):  # one result per tree, errors in forest numbering
+            f = sets[0]
+            res = [O.eval_batch([t.rs], arena, offs, lens) for t in f.trees]
+            tri = np.stack([r[0] for r in res], axis=1)
+            err = np.stack([np.where(r[1] >= 0, r[1] + o, r[1]) for r, o in zip(res, f.offsets)], axis=1)
+            return tri, err, None
         tri, err, bm = O.eval_batch([s.rs for s in sets], arena, offs, lens, set_of_req=set_of_req)
         return tri, err, (bm if with_bitmap else None)
 
@@ -111,7 +131,7 @@ def test_priorities_and_first_denial():
     assert res[0].authorization == {"p0-ok": True, "p0-deny": True, "p0-nil": True}
     # request 1 is denied at priority 0; priority 1 never runs for it
     assert res[1].code == P.CODE_PERMISSION_DENIED and res[1].denied_by == "p0-deny"
-    assert ctx.launches == 2  # one device launch per priority level
+    assert ctx.launches == 1  # one forest launch: no later priority reads auth.authorization.*
 
 
 def test_later_priority_reads_earlier_authorization():
