@@ -80,6 +80,35 @@ int ensure_sets(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_s
     return AUTHJX_OK;
 }
 
+// capture rows, slow list and request order for a batch of n on stream s (grown when
+// needed: no batch in flight on this context may still use the old buffers)
+int ensure_work(authjx_ctx* ctx, uint32_t n, uint32_t row_stride, hipStream_t s) {
+    if (n <= ctx->slow_cap && n <= ctx->perm_cap && (size_t)n * row_stride <= ctx->rows_cap) return AUTHJX_OK;
+    HIP_OK(hipStreamSynchronize(s));
+    if (n > ctx->slow_cap) {
+        if (ctx->d_slow) (void)hipFree(ctx->d_slow);
+        ctx->d_slow = nullptr;
+        ctx->slow_cap = 0;
+        HIP_OK(hipMalloc(&ctx->d_slow, ((size_t)n + 1) * sizeof(uint32_t)));
+        ctx->slow_cap = n;
+    }
+    if (n > ctx->perm_cap) {
+        if (ctx->d_perm) (void)hipFree(ctx->d_perm);
+        ctx->d_perm = nullptr;
+        ctx->perm_cap = 0;
+        HIP_OK(hipMalloc(&ctx->d_perm, ((size_t)n + 2048) * sizeof(uint32_t)));
+        ctx->perm_cap = n;
+    }
+    if ((size_t)n * row_stride > ctx->rows_cap) {
+        if (ctx->d_rows) (void)hipFree(ctx->d_rows);
+        ctx->d_rows = nullptr;
+        ctx->rows_cap = 0;
+        HIP_OK(hipMalloc(&ctx->d_rows, (size_t)n * row_stride * sizeof(uint64_t)));
+        ctx->rows_cap = (size_t)n * row_stride;
+    }
+    return AUTHJX_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -215,30 +244,9 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     HIP_OK(hipSetDevice(ctx->device));
     int rc = ensure_sets(ctx, sets, n_sets, s);
     if (rc != AUTHJX_OK) return rc;
-    if (!ctx->force_scan && (n > ctx->slow_cap || n > ctx->perm_cap || (size_t)n * row_stride > ctx->rows_cap)) {
-        // growing the work buffers: no batch in flight on this context may still use them
-        HIP_OK(hipStreamSynchronize(s));
-        if (n > ctx->slow_cap) {
-            if (ctx->d_slow) (void)hipFree(ctx->d_slow);
-            ctx->d_slow = nullptr;
-            ctx->slow_cap = 0;
-            HIP_OK(hipMalloc(&ctx->d_slow, ((size_t)n + 1) * sizeof(uint32_t)));
-            ctx->slow_cap = n;
-        }
-        if (n > ctx->perm_cap) {
-            if (ctx->d_perm) (void)hipFree(ctx->d_perm);
-            ctx->d_perm = nullptr;
-            ctx->perm_cap = 0;
-            HIP_OK(hipMalloc(&ctx->d_perm, ((size_t)n + 2048) * sizeof(uint32_t)));
-            ctx->perm_cap = n;
-        }
-        if ((size_t)n * row_stride > ctx->rows_cap) {
-            if (ctx->d_rows) (void)hipFree(ctx->d_rows);
-            ctx->d_rows = nullptr;
-            ctx->rows_cap = 0;
-            HIP_OK(hipMalloc(&ctx->d_rows, (size_t)n * row_stride * sizeof(uint64_t)));
-            ctx->rows_cap = (size_t)n * row_stride;
-        }
+    if (!ctx->force_scan) {
+        rc = ensure_work(ctx, n, row_stride, s);
+        if (rc != AUTHJX_OK) return rc;
     }
     HIP_OK(hipEventRecord(ctx->ev0, s));
     if (ctx->force_scan)
@@ -272,15 +280,29 @@ int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* set
         return AUTHJX_EINVAL;
     if (n_sets > 1 && !d_set_of_req) return AUTHJX_EINVAL;
     if (n_sets == 1) d_set_of_req = nullptr;
-    for (uint32_t i = 0; i < n_sets; i++)
+    uint32_t max_sel = 0;
+    for (uint32_t i = 0; i < n_sets; i++) {
         if (!sets[i] || sets[i]->c.n_patterns > values_stride) return AUTHJX_EINVAL;
+        if (sets[i]->c.n_selectors > max_sel) max_sel = sets[i]->c.n_selectors;
+    }
+    const uint32_t row_stride = 1 + max_sel;
     std::lock_guard<std::mutex> lock(ctx->mu);
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     HIP_OK(hipSetDevice(ctx->device));
     int rc = ensure_sets(ctx, sets, n_sets, s);
     if (rc != AUTHJX_OK) return rc;
-    HIP_OK(ajx::launch_select(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n,
-                              reinterpret_cast<uint32_t*>(d_out_values), values_stride, s));
+    const bool exact = ctx->force_scan != 0;  // the exact Get per selector (cross-check)
+    if (!exact && (rc = ensure_work(ctx, n, row_stride, s)) != AUTHJX_OK) return rc;
+    const uint32_t* perm = nullptr;
+    if (!exact && ctx->len_sort && n_sets == 1 && n >= 4096) {
+        HIP_OK(ajx::launch_len_order(d_lens, n, ctx->d_perm + n, ctx->d_perm, s));
+        perm = ctx->d_perm;
+    }
+    const uint32_t shared_bytes =
+        (n_sets == 1 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes) ? (uint32_t)sets[0]->c.blob.size() : 0u;
+    HIP_OK(ajx::launch_select(ctx->d_sets, d_set_of_req, shared_bytes, d_arena, d_offs, d_lens, n,
+                              reinterpret_cast<uint32_t*>(d_out_values), values_stride,
+                              exact ? nullptr : ctx->d_rows, row_stride, ctx->d_slow, ctx->d_slow + 1, perm, s));
     return AUTHJX_OK;
 }
 

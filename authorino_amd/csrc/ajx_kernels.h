@@ -9,10 +9,14 @@ hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
                             int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream);
 
-// gjson.Get of every pattern's selector: d_out = u32[n][stride][3] {start, len, type | esc << 8}
-hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
-                         const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint32_t* d_out,
-                         uint32_t stride, hipStream_t stream);
+// gjson.Get of every pattern's selector: d_out = u32[n][stride][3] {start, len, type | esc << 8}.
+// With d_rows: the single-pass stage A captures all spans in one scan per document (rows of
+// 1 + n_selectors u64, requests it can not prove go through the exact Get); without, the
+// exact Get per selector.
+hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
+                         const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                         uint32_t* d_out, uint32_t stride, uint64_t* d_rows, uint32_t row_stride,
+                         uint32_t* d_slow_count, uint32_t* d_slow_ids, const uint32_t* d_perm, hipStream_t stream);
 
 }  // namespace ajx
 

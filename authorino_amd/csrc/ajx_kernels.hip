@@ -222,10 +222,12 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fast(cons
                                                      const uint32_t* __restrict__ lens, uint32_t n,
                                                      uint64_t* __restrict__ rows, uint32_t row_stride,
                                                      uint32_t* __restrict__ slow_count,
-                                                     uint32_t* __restrict__ slow_ids, uint32_t ring_off) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : (r < n ? set_of_req[r] : 0)]);
-    if (r >= n) return;
+                                                     uint32_t* __restrict__ slow_ids, uint32_t ring_off,
+                                                     const uint32_t* __restrict__ perm) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t r = k < n ? (perm ? perm[k] : k) : 0u;
+    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : set_of_req[r]]);
+    if (k >= n) return;
     if (!scan_request<MODE>(blob, arena + offs[r], lens[r], rows + (size_t)r * row_stride, lane_ring(ring_off)))
         slow_ids[atomicAdd(slow_count, 1u)] = r;
 }
@@ -465,9 +467,13 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
                                                          const uint8_t* __restrict__ arena,
                                                          const uint64_t* __restrict__ offs,
                                                          const uint32_t* __restrict__ lens, uint32_t n,
-                                                         uint32_t* __restrict__ out, uint32_t stride) {
+                                                         uint32_t* __restrict__ out, uint32_t stride,
+                                                         const uint64_t* __restrict__ rows, uint32_t row_stride) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
+    // the single-pass scan's capture row when it has one (not on the slow list)
+    const uint64_t* row = rows ? rows + (size_t)r * row_stride : nullptr;
+    const uint64_t found = row ? row[0] : kRowSlow;
     const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const Selector* sels = reinterpret_cast<const Selector*>(blob + h->off_selectors);
@@ -485,7 +491,22 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
             o[2] = 0xFFu;
             continue;
         }
-        const Selector& sl = sels[pats[p].selector];
+        const uint32_t si = pats[p].selector;
+        if (!(found & kRowSlow)) {
+            if ((found >> si) & 1u) {
+                const uint64_t rec = row[1 + si];
+                const uint32_t meta = (uint32_t)(rec >> 32);
+                o[0] = (uint32_t)rec;
+                o[1] = meta & 0xFFFFFFu;
+                o[2] = ((meta >> 24) & 7u) | (((meta >> 27) & 1u) << 8);
+            } else {
+                o[0] = 0;
+                o[1] = 0;
+                o[2] = T_NULL;
+            }
+            continue;
+        }
+        const Selector& sl = sels[si];
         const ValueRef v = gj_get(doc, len, comps + sl.comp_begin, sl.comp_count, lits);
         o[0] = v.start;
         o[1] = v.end - v.start;
@@ -493,14 +514,42 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
     }
 }
 
-hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
-                         const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint32_t* d_out,
-                         uint32_t stride, hipStream_t stream) {
+hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
+                         const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                         uint32_t* d_out, uint32_t stride, uint64_t* d_rows, uint32_t row_stride,
+                         uint32_t* d_slow_count, uint32_t* d_slow_ids, const uint32_t* d_perm, hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    if (d_rows) {  // stage A of the single-pass kernel captures every selector's span
+        const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
+        const uint32_t fblock = shared && shared_blob_bytes <= 8192 ? 256u : kFastBlock;
+        const uint32_t fgrid = (n + fblock - 1) / fblock;
+        const uint32_t ring_off = shared ? (shared_blob_bytes + 15u) & ~15u : 0u;
+        const uint32_t lds = ring_off + (fblock / 64) * kWinRingBytesPerWave;
+        hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        static bool attr_set = false;
+        if (!attr_set) {
+            const void* ks[] = {reinterpret_cast<const void*>(&ajx_scan_fast<0, true>),
+                                reinterpret_cast<const void*>(&ajx_scan_fast<0, false>)};
+            for (const void* k : ks)
+                if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
+                    return e;
+            attr_set = true;
+        }
+        if (shared)
+            hipLaunchKernelGGL((ajx_scan_fast<0, true>), dim3(fgrid), dim3(fblock), lds, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off,
+                               d_perm);
+        else
+            hipLaunchKernelGGL((ajx_scan_fast<0, false>), dim3(fgrid), dim3(fblock), lds, stream, d_sets,
+                               d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids,
+                               ring_off, d_perm);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
     hipLaunchKernelGGL(ajx_select_values, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                       d_lens, n, d_out, stride);
+                       d_lens, n, d_out, stride, d_rows, row_stride);
     return hipGetLastError();
 }
 
@@ -548,10 +597,10 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
         if (!shared) return hipErrorInvalidValue;
         if (mode == 1)
             hipLaunchKernelGGL((ajx_scan_fast<1, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off);
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off, nullptr);
         else
             hipLaunchKernelGGL((ajx_scan_fast<2, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off);
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off, nullptr);
         return hipGetLastError();
     }
     if (mode == 5 || mode >= 10) {  // the line engine; 11/12/13 profiling ablations
@@ -580,13 +629,13 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     } else if (mode == 3) {  // profiling split: stage A and stage B as two launches
         if (shared) {
             hipLaunchKernelGGL((ajx_scan_fast<0, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off);
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off, nullptr);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             hipLaunchKernelGGL((ajx_patterns<true>), dim3(grid), dim3(block), ring_off, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
         } else {
             hipLaunchKernelGGL((ajx_scan_fast<0, false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off);
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off, nullptr);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             hipLaunchKernelGGL((ajx_patterns<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);

@@ -225,6 +225,17 @@ class Context:
             return tri.reshape(-1, nt)[:n], err.reshape(-1, nt)[:n], (bm[:n] if bm is not None else None)
         return tri[:n], err[:n], (bm[:n] if bm is not None else None)
 
+    def select_device(self, sets, arena, offs, lens, out, set_of_req=None, stream=None) -> None:
+        """authjx_select_batch_device on HBM-resident torch tensors; out: u32[n][stride][3].
+        Asynchronous."""
+        n = int(lens.numel())
+        sarr = (C.c_void_p * len(sets))(*[s._h.value for s in sets])
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        rc = load_library().authjx_select_batch_device(
+            self._h, sarr, len(sets), ptr(set_of_req), ptr(arena), ptr(offs), ptr(lens), n, ptr(out),
+            int(out.shape[1]), C.c_void_p(stream) if stream else None)
+        _check(rc, "authjx_select_batch_device")
+
     def select_host_arena(self, sets, arena, offs, lens, set_of_req=None) -> np.ndarray:
         """gjson.Get of every pattern selector of each request's ruleset on the device
         (authjx_select_batch): u32[n][stride][3] = {start, len, type | esc << 8}."""

@@ -78,6 +78,32 @@ def cpu_baseline(w, rpr, target_s, gpu_tri, gpu_bm):
     }, {"sample": sample, "mismatches": mism}
 
 
+def phase_cpu_baseline(w, exprs, target_s, gpu_tri):
+    """c5: the oracle evaluates every tree of the phase (re-scanning the document per
+    pattern, like the reference) on a bounded prefix; parity of the per-tree results."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    rss = [pyoracle.Ruleset.from_expression(e) for e in exprs]
+    R = sum(len(e.flatten()[0]) for e in exprs)
+    k = min(w.n, 4096)
+    t0 = time.perf_counter()
+    outs = [pyoracle.eval_batch([r], w.arena, w.offs[:k], w.lens[:k], nthreads=threads)[0] for r in rss]
+    dt = time.perf_counter() - t0
+    if dt < target_s:
+        k = int(min(w.n, k * target_s / max(dt, 1e-6)))
+        t0 = time.perf_counter()
+        outs = [pyoracle.eval_batch([r], w.arena, w.offs[:k], w.lens[:k], nthreads=threads)[0] for r in rss]
+        dt = time.perf_counter() - t0
+    got = np.stack(outs, axis=1)
+    mism = int((got != gpu_tri[:k]).any(axis=1).sum())
+    return {"value": k * R / dt, "unit": "request×rule evals/s", "decisions_per_s": k / dt, "cores": threads,
+            "kind": "port", "sample": f"first {k} of the {w.n} docs, every tree of the phase, oracle/ C restatement, "
+                                      f"{threads} host threads, {dt:.1f}s"}, {"sample": k, "mismatches": mism}
+
+
 def timed_steps(step, steps, warmup, dist, torch, dev, stream=None):
     """W untimed steps, then exactly K timed steps bracketed by barrier + synchronize on
     both sides; returns (wall seconds, mean per-step event ms on `stream`), each the max
@@ -135,19 +161,34 @@ def main():
     from authorino_amd import runtime, workloads
 
     w = workloads.make(args.workload, n=args.n, seed=1000 + rank)
-    rpr = w.patterns_per_request()  # R of each request's rule set
-    R = int(max(len(e.flatten()[0]) for e in w.sets))
     ctx = runtime.Context(local)
-    rss = [ctx.compile_expression(e) for e in w.sets]
+    phase = w.auth_config is not None  # c5: the whole authorization phase per request
+    if phase:
+        # one forest ruleset (top-level when, each evaluator's when and rules: one scan per
+        # document) + the response-header selectors (authjx_select_batch_device)
+        from authorino_amd.response import ResponseSelectors
+
+        cfg = w.auth_config
+        exprs = [cfg.conditions] + [e for c in cfg.authorization for e in (c.conditions, c.rules)]
+        rss = [ctx.compile_forest(exprs)]
+        sel = ResponseSelectors(cfg.response, ctx)
+        R = rss[0].n_patterns
+        rpr = np.full(w.n, R, dtype=np.int64)
+    else:
+        rpr = w.patterns_per_request()  # R of each request's rule set
+        R = int(max(len(e.flatten()[0]) for e in w.sets))
+        rss = [ctx.compile_expression(e) for e in w.sets]
 
     arena = torch.from_numpy(w.arena).to(dev)
     offs = torch.from_numpy(w.offs.view(np.int64)).to(dev)
     lens = torch.from_numpy(w.lens.view(np.int32)).to(dev)
     sor = torch.from_numpy(w.set_of_req.view(np.int32)).to(dev) if w.set_of_req is not None else None
     words = (R + 63) // 64
-    tri = torch.empty(w.n, dtype=torch.uint8, device=dev)
-    err = torch.empty(w.n, dtype=torch.int32, device=dev)
+    nt = rss[0].n_trees
+    tri = torch.empty(w.n * nt, dtype=torch.uint8, device=dev)
+    err = torch.empty(w.n * nt, dtype=torch.int32, device=dev)
     bm = torch.empty((w.n, words), dtype=torch.int64, device=dev)
+    spans = torch.empty((w.n, len(sel.paths), 3), dtype=torch.int32, device=dev) if phase else None
     # a dedicated (non-null) stream: the kernel and the timing events share it
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
@@ -155,12 +196,18 @@ def main():
 
     def step():
         ctx.eval_device(rss, arena, offs, lens, tri, err, bm, set_of_req=sor, stream=sp)
+        if phase:
+            ctx.select_device([sel.ruleset], arena, offs, lens, spans, stream=sp)
 
     elapsed, kern_ms = timed_steps(step, args.steps, args.warmup, dist, torch, dev, stream)
 
     total_req = w.n * args.steps * world
     value = int(rpr.sum()) * args.steps * world / elapsed  # shards are equal-sized (weak scaling)
-    algo_bytes = int(w.lens.astype(np.int64).sum()) + int(((rpr + 7) // 8 + 1).sum())
+    # doc read once + pattern bitmap + one result byte per tree (+ 12-B spans of the response
+    # selectors for c5)
+    algo_bytes = int(w.lens.astype(np.int64).sum()) + int(((rpr + 7) // 8 + nt).sum())
+    if phase:
+        algo_bytes += w.n * len(sel.paths) * 12
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     try:
@@ -172,7 +219,19 @@ def main():
         pass
 
     cpu, parity = None, None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    extra = {}
+    if phase:
+        # the phase decision from the per-tree results (auth_pipeline.go:454-457, :287-322)
+        t = tri.cpu().numpy().reshape(w.n, nt)
+        skipped = t[:, 0] != runtime.T
+        ok = np.ones(w.n, dtype=bool)
+        for k in range(len(cfg.authorization)):
+            ok &= (t[:, 1 + 2 * k] != runtime.T) | (t[:, 2 + 2 * k] == runtime.T)
+        extra = {"phase": {"trees": nt, "skipped": int(skipped.sum()), "allowed": int((skipped | ok).sum()),
+                           "response_selectors": len(sel.paths)}}
+        if rank == 0 and world == 1 and not args.no_cpu:
+            cpu, parity = phase_cpu_baseline(w, exprs, args.cpu_seconds, t)
+    elif rank == 0 and world == 1 and not args.no_cpu:
         cpu, parity = cpu_baseline(w, rpr, args.cpu_seconds, tri.cpu().numpy(), bm.cpu().numpy().view(np.uint64))
     undecided = int((tri == runtime.UNDECIDED).sum().item())
     exact_path = ctx.last_exact_count()  # requests the single-pass kernel handed to the exact scan
@@ -199,6 +258,7 @@ def main():
                 "patterns": R if w.set_of_req is None else float(rpr.mean()),
                 "selectors": rss[0].n_selectors if len(rss) == 1 else float(np.mean([r.n_selectors for r in rss])),
                 "auth_configs": len(rss),
+                "trees_per_request": nt,
                 "doc_bytes_mean": float(w.lens.mean()),
                 "parallelism": f"dp{world} (independent request shards, no collective)",
             },
@@ -215,6 +275,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "undecided": undecided,
+            **extra,
             "exact_path_requests": exact_path,
         }
         print(json.dumps(line), flush=True)

@@ -331,6 +331,18 @@ def test_select_values_match_oracle(ctx):
         t, st, ln = O.gjson_span(d, p)
         g = got[k, 0]
         assert (int(g[2]) & 0xFF, int(g[0]), int(g[1])) == (t, st, ln), (d[:200], p)
+    # one ruleset of all C5 response paths (LDS-staged single-pass scan, length-ordered)
+    w = workloads.make("c5", n=8192, seed=55)
+    rs = ctx.compile([(p, 1, "") for p in sel5], [], -1)
+    got = ctx.select_host_arena([rs], w.arena, w.offs, w.lens)
+    ctx.set_exact_scan(True)
+    exact = ctx.select_host_arena([rs], w.arena, w.offs, w.lens)
+    ctx.set_exact_scan(False)
+    assert np.array_equal(got[:, :, :2], exact[:, :, :2]) and np.array_equal(got[:, :, 2] & 0xFF, exact[:, :, 2] & 0xFF)
+    for i in range(0, w.n, 97):
+        for j, p in enumerate(sel5):
+            t, st, ln = O.gjson_span(w.doc(i), p)
+            assert (int(got[i, j, 2]) & 0xFF, int(got[i, j, 0]), int(got[i, j, 1])) == (t, st, ln)
 
 
 def test_c5_full_phase_on_device(ctx):
