@@ -37,7 +37,7 @@ struct authjx_ctx {
     uint32_t slow_cap = 0;
     uint64_t* d_rows = nullptr;  // stage-A capture rows
     size_t rows_cap = 0;         // in u64
-    uint32_t* d_perm = nullptr;  // length-bucketed request order (+ 2 x 1024 u32 histogram)
+    uint32_t* d_perm = nullptr;  // length-bucketed request order (+ 2 x 1024 + 1 u32 histogram)
     uint32_t perm_cap = 0;
     int len_sort = 1;            // order requests by length class before the single-pass kernel
     int force_scan = 0;
@@ -96,7 +96,7 @@ int ensure_work(authjx_ctx* ctx, uint32_t n, uint32_t row_stride, hipStream_t s)
         if (ctx->d_perm) (void)hipFree(ctx->d_perm);
         ctx->d_perm = nullptr;
         ctx->perm_cap = 0;
-        HIP_OK(hipMalloc(&ctx->d_perm, ((size_t)n + 2048) * sizeof(uint32_t)));
+        HIP_OK(hipMalloc(&ctx->d_perm, ((size_t)n + 4096) * sizeof(uint32_t)));
         ctx->perm_cap = n;
     }
     if ((size_t)n * row_stride > ctx->rows_cap) {

@@ -796,10 +796,27 @@ AJX_HD bool incl_hits(const uint8_t* doc, const ValueRef& v, const Pattern* pats
         }
         const RawVal r = raw_value(doc, e);
         if (!r.ok) return false;
-        for (uint32_t j = 0; j < cnt; j++) {
-            const Pattern pt = pats[plist[begin + j]];
-            if ((pt.op == OP_INCL || pt.op == OP_EXCL) && pt.state == P_OK && raw_equals(doc, r, pt, lits))
-                h |= 1u << j;
+        if (!r.lit && r.n <= 8) {
+            // a short element (the common case: group / role names): its bytes are read
+            // from the document once, into two masked dwords, and compared with each
+            // literal's dwords (4-byte aligned in the pool, LDS when the blob is staged)
+            const uint32_t n0 = r.n < 4 ? r.n : 4u, n1 = r.n - n0;
+            const uint32_t m0 = n0 == 4 ? 0xFFFFFFFFu : (1u << (8 * n0)) - 1u;
+            const uint32_t m1 = n1 == 4 ? 0xFFFFFFFFu : (1u << (8 * n1)) - 1u;
+            const uint32_t w0 = n0 ? load_u32_upto(doc + r.a, n0) & m0 : 0u;
+            const uint32_t w1 = n1 ? load_u32_upto(doc + r.a + 4, n1) & m1 : 0u;
+            for (uint32_t j = 0; j < cnt; j++) {
+                const Pattern pt = pats[plist[begin + j]];
+                if ((pt.op != OP_INCL && pt.op != OP_EXCL) || pt.state != P_OK || pt.lit_len != r.n) continue;
+                const uint32_t* lw = reinterpret_cast<const uint32_t*>(lits + pt.lit_off);
+                if ((lw[0] & m0) == w0 && (n1 == 0 || (lw[1] & m1) == w1)) h |= 1u << j;
+            }
+        } else {
+            for (uint32_t j = 0; j < cnt; j++) {
+                const Pattern pt = pats[plist[begin + j]];
+                if ((pt.op == OP_INCL || pt.op == OP_EXCL) && pt.state == P_OK && raw_equals(doc, r, pt, lits))
+                    h |= 1u << j;
+            }
         }
         i = e.end;
         if (i < end) {

@@ -39,7 +39,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             int mode = 0, const uint32_t* d_perm = nullptr);
 
 // Length-bucketed request order for the single-pass kernel: d_perm[n] = request ids,
-// longest 8-byte length class first; d_hist needs 2 * 1024 u32 of scratch.
+// longest 8-byte length class first; d_hist needs 2 * 1024 + 1 u32 of scratch.
 hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist, uint32_t* d_perm,
                             hipStream_t stream);
 

@@ -408,14 +408,27 @@ __global__ __launch_bounds__(kLenBuckets) void ajx_len_hist(const uint32_t* __re
     if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
 
-// exclusive scan of the histogram into per-class cursors (one workgroup)
+// exclusive scan of the histogram into per-class cursors (one workgroup).
+// cursor[kLenBuckets] = 1 when the lengths span fewer than kLenSpreadMin classes: the
+// order would not even out the waves (and scatters the outputs), so the scatter writes
+// the identity instead.
+constexpr uint32_t kLenSpreadMin = 32;  // 256 bytes
 __global__ __launch_bounds__(kLenBuckets) void ajx_len_scan(const uint32_t* __restrict__ hist,
                                                             uint32_t* __restrict__ cursor) {
     __shared__ uint32_t s[kLenBuckets];
+    __shared__ uint32_t lo, hi;
     const uint32_t t = threadIdx.x;
     const uint32_t own = hist[t];
+    if (t == 0) {
+        lo = kLenBuckets;
+        hi = 0;
+    }
     s[t] = own;
     __syncthreads();
+    if (own) {
+        atomicMin(&lo, t);
+        atomicMax(&hi, t);
+    }
     for (uint32_t o = 1; o < kLenBuckets; o <<= 1) {
         const uint32_t v = t >= o ? s[t - o] : 0u;
         __syncthreads();
@@ -423,6 +436,7 @@ __global__ __launch_bounds__(kLenBuckets) void ajx_len_scan(const uint32_t* __re
         __syncthreads();
     }
     cursor[t] = s[t] - own;
+    if (t == 0) cursor[kLenBuckets] = (hi < lo || hi - lo < kLenSpreadMin) ? 1u : 0u;
 }
 
 // perm[cursor[class] + rank] = request; one global atomic per (workgroup, class)
@@ -431,9 +445,13 @@ __global__ __launch_bounds__(kLenBuckets) void ajx_len_scatter(const uint32_t* _
                                                                uint32_t* __restrict__ perm) {
     __shared__ uint32_t cnt[kLenBuckets];
     __shared__ uint32_t base[kLenBuckets];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cursor[kLenBuckets]) {  // narrow length spread: keep the caller's order
+        if (i < n) perm[i] = i;
+        return;
+    }
     cnt[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t b = 0, rank = 0;
     if (i < n) {
         b = len_bucket(lens[i]);
@@ -447,7 +465,7 @@ __global__ __launch_bounds__(kLenBuckets) void ajx_len_scatter(const uint32_t* _
 
 hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist, uint32_t* d_perm,
                             hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(d_hist, 0, 2 * kLenBuckets * sizeof(uint32_t), stream);
+    hipError_t e = hipMemsetAsync(d_hist, 0, (2 * kLenBuckets + 1) * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     const uint32_t blocks = (n + kLenBuckets - 1) / kLenBuckets;
     hipLaunchKernelGGL(ajx_len_hist, dim3(blocks < 512 ? blocks : 512), dim3(kLenBuckets), 0, stream, d_lens, n,

@@ -21,7 +21,11 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 w = workloads.make(wl, n=n)
 ctx = runtime.Context(0)
-rss = [ctx.compile_expression(e) for e in w.sets]
+if w.auth_config is not None:  # c5: the phase's forest ruleset
+    cfg = w.auth_config
+    rss = [ctx.compile_forest([cfg.conditions] + [e for c in cfg.authorization for e in (c.conditions, c.rules)])]
+else:
+    rss = [ctx.compile_expression(e) for e in w.sets]
 sor = torch.from_numpy(w.set_of_req.view(np.int32)).to(dev) if w.set_of_req is not None else None
 L = runtime.load_library()
 L.authjx_debug_ablate.argtypes = [C.c_void_p, C.c_int]
@@ -29,9 +33,9 @@ L.authjx_debug_len_sort.argtypes = [C.c_void_p, C.c_int]
 arena = torch.from_numpy(w.arena).to(dev)
 offs = torch.from_numpy(w.offs.view(np.int64)).to(dev)
 lens = torch.from_numpy(w.lens.view(np.int32)).to(dev)
-R = max(len(e.flatten()[0]) for e in w.sets)
-tri = torch.empty(n, dtype=torch.uint8, device=dev)
-err = torch.empty(n, dtype=torch.int32, device=dev)
+R = max(r.n_patterns for r in rss)
+tri = torch.empty(n * rss[0].n_trees, dtype=torch.uint8, device=dev)
+err = torch.empty(n * rss[0].n_trees, dtype=torch.int32, device=dev)
 bm = torch.empty((n, (R + 63) // 64), dtype=torch.int64, device=dev)
 stream = torch.cuda.Stream(dev)
 torch.cuda.set_stream(stream)
