@@ -358,6 +358,18 @@ struct Scan {
         }
     }
 
+    // a string value closed at block offset i (state X_VALUE / X_VALUE_OR_CLOSE)
+    AJX_HD void value_string(uint32_t i) {
+        const int32_t s = leaf_sel(value_node());
+        if (s >= 0) {
+            const uint32_t so = open_before(i);
+            const uint32_t lb = last_bs_before(i);
+            record(s, so, (uint32_t)(bpos + (int32_t)i) + 1, T_STRING, (lb != ~0u && lb > so) ? 1u : 0u);
+        }
+        element_done();
+        st = X_COMMA_OR_CLOSE;
+    }
+
     // one token at block offset i (byte c). Strings arrive as one token, their closing
     // quote (nothing inside a string is a token, so the state before the opening quote
     // still holds there).
@@ -395,14 +407,7 @@ struct Scan {
             case X_VALUE:
             case X_VALUE_OR_CLOSE:
                 if (c == '"') {
-                    const int32_t s = leaf_sel(value_node());
-                    if (s >= 0) {
-                        const uint32_t so = open_before(i);
-                        const uint32_t lb = last_bs_before(i);
-                        record(s, so, p + 1, T_STRING, (lb != ~0u && lb > so) ? 1u : 0u);
-                    }
-                    element_done();
-                    st = X_COMMA_OR_CLOSE;
+                    value_string(i);
                     return;
                 }
                 if (c == '{' || c == '[') {
@@ -521,7 +526,8 @@ struct Scan {
             token(byte_at(i), i);
             if (st >= X_DONE) return;
             // compact JSON: the ':' right after a key and the ',' right after a value are
-            // taken in the same iteration
+            // taken in the same iteration, and so is a member's string value that opens
+            // right after its ':' ("key":"value", — one iteration per member)
             const uint32_t nb = i + 1;
             if (nb < 64 && ((toks >> nb) & 1u)) {
                 const uint32_t c2 = byte_at(nb);
@@ -531,6 +537,20 @@ struct Scan {
                     st = (colon || top_is_arr()) ? X_VALUE : X_KEY;
                     toks &= toks - 1;
                     below = below64f(nb + 1);
+                    // the opening quote right after the ':' and its closing quote in this
+                    // window (nothing inside a string is a token: it is the next token)
+                    if (colon && nb + 1 < 64 && ((oq >> (nb + 1)) & 1u) && toks) {
+                        const uint32_t j = ctz64f(toks);
+                        toks &= toks - 1;
+                        below = below64f(j + 1);
+                        value_string(j);
+                        const uint32_t nb2 = j + 1;
+                        if (nb2 < 64 && ((toks >> nb2) & 1u) && byte_at(nb2) == ',') {
+                            st = top_is_arr() ? X_VALUE : X_KEY;
+                            toks &= toks - 1;
+                            below = below64f(nb2 + 1);
+                        }
+                    }
                 }
             }
         }
