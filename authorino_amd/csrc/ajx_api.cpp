@@ -4,6 +4,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -40,6 +41,7 @@ struct authjx_ctx {
     uint32_t* d_perm = nullptr;  // length-bucketed request order (+ 2 x 1024 + 1 u32 histogram)
     uint32_t perm_cap = 0;
     int len_sort = 1;            // order requests by length class before the single-pass kernel
+    int no_tenant_stage = 0;     // profiling: multi-tenant batches read tables from global memory
     int force_scan = 0;
     int ablate = 0;  // profiling only: run a reduced stage A (1 loads, 2 loads+classify)
     float last_ms = 0.f;
@@ -260,9 +262,15 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
             HIP_OK(ajx::launch_len_order(d_lens, n, ctx->d_perm + n, ctx->d_perm, s));
             perm = ctx->d_perm;
         }
+        // uniform batch: the blob staged once per workgroup; multi-tenant batch: the largest
+        // blob, for workgroups whose requests share one ruleset (ajx_scan_fused_tenant)
+        size_t max_blob = 0;
+        for (uint32_t i = 0; i < n_sets; i++) max_blob = std::max(max_blob, sets[i]->c.blob.size());
+        const uint32_t stage_bytes =
+            n_sets == 1 ? (max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u)
+                        : (!ctx->no_tenant_stage && max_blob <= ajx::kMaxTenantStageBytes ? (uint32_t)max_blob : 0u);
         HIP_OK(ajx::launch_eval_fast(
-            ctx->d_sets, d_set_of_req,
-            (n_sets == 1 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes) ? (uint32_t)sets[0]->c.blob.size() : 0u,
+            ctx->d_sets, d_set_of_req, stage_bytes,
             d_arena, d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words, ctx->d_rows,
             row_stride, ctx->d_slow, ctx->d_slow + 1, s, ctx->ablate, perm));
     }
@@ -365,6 +373,15 @@ int authjx_debug_len_sort(authjx_ctx* ctx, int on) {
     if (!ctx) return AUTHJX_EINVAL;
     std::lock_guard<std::mutex> lock(ctx->mu);
     ctx->len_sort = on;  // 0 off, 1 single-ruleset batches, 2 also multi-tenant batches
+    return AUTHJX_OK;
+}
+
+// Profiling only (not in authjx.h): workgroup-uniform LDS staging of multi-tenant
+// rulesets on (1, default) or off (0: every table read from global memory).
+int authjx_debug_tenant_stage(authjx_ctx* ctx, int on) {
+    if (!ctx) return AUTHJX_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->no_tenant_stage = on ? 0 : 1;
     return AUTHJX_OK;
 }
 

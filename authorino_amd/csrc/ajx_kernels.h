@@ -24,6 +24,9 @@ namespace ajx {
 
 // Largest ruleset blob the kernels stage into LDS (a batch over one ruleset).
 constexpr uint32_t kMaxSharedBlobBytes = 48 * 1024;
+// multi-tenant batches: the largest blob a 4-wave workgroup stages in LDS next to its
+// window rings (blob + 4 x 8 KiB rings per group keeps 4 groups = 4 waves/SIMD per CU)
+constexpr uint32_t kMaxTenantStageBytes = 8 * 1024;
 
 // single-pass kernel + exact scan of the requests it hands over (d_slow_count is zeroed
 // on the stream first; d_slow_ids needs room for n entries). shared_blob_bytes: the

@@ -278,6 +278,46 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused(con
     finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride);
 }
 
+// The single-pass kernel for multi-tenant batches (one ruleset per request through
+// set_of_req; the caller buckets requests by AuthConfig). A workgroup whose requests all
+// use one ruleset copies that blob into LDS, as the uniform-ruleset kernel does, so its
+// table reads are ds_reads; a workgroup straddling two buckets reads the tables from
+// global memory. Dynamic LDS: [blob copy (up to stage_cap bytes)] [window rings].
+__global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_tenant(
+    const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
+    uint64_t* __restrict__ rows, uint32_t row_stride, uint32_t* __restrict__ slow_count,
+    uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+    uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t ring_off, const uint32_t* __restrict__ perm) {
+    const uint32_t k0 = blockIdx.x * blockDim.x;  // (< n: the grid covers n)
+    const uint32_t k = k0 + threadIdx.x;
+    const uint32_t r0 = perm ? perm[k0] : k0;
+    const uint32_t r = k < n ? (perm ? perm[k] : k) : r0;
+    const uint32_t sid0 = set_of_req[r0], sid = set_of_req[r];
+    const uint8_t* gblob = sets[sid];
+    // (block-uniform: every thread reaches the barrier in stage_blob or none does)
+    const bool uni = __syncthreads_and(sid == sid0) &&
+                     reinterpret_cast<const RulesetHdr*>(sets[sid0])->total_bytes <= ring_off;
+    uint64_t* row = rows + (size_t)r * row_stride;
+    const uint8_t* d = arena + offs[r];
+    if (uni) {
+        const uint8_t* blob = stage_blob<true>(gblob);
+        if (k >= n) return;
+        if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off))) {
+            slow_ids[atomicAdd(slow_count, 1u)] = r;
+            return;
+        }
+        finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride);
+    } else {
+        if (k >= n) return;
+        if (!scan_request<0>(gblob, d, lens[r], row, lane_ring(ring_off))) {
+            slow_ids[atomicAdd(slow_count, 1u)] = r;
+            return;
+        }
+        finish_request(r, gblob, d, row, out_tri, out_err, out_bm, stride);
+    }
+}
+
 // The line engine. Dynamic LDS: [blob copy (SHARED)] [ring: 4 waves x 16 KiB]. Every
 // thread reaches the staging barrier before any exits.
 constexpr uint32_t kLinesBlock = 256;
@@ -609,6 +649,12 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
         for (const void* k : ks)
             if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
                 return e;
+        // (the tenant kernel also holds static LDS for __syncthreads_and: ask only for what
+        // its launch uses, blob + four window rings)
+        if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ajx_scan_fused_tenant),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     kMaxTenantStageBytes + 4 * kWinRingBytesPerWave)) != hipSuccess)
+            return e;
         fast_attr_set = true;
     }
     if (mode == 1 || mode == 2) {  // profiling ablations of stage A (uniform ruleset only)
@@ -662,6 +708,14 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
         hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
                            d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
                            stride, ring_off, d_perm);
+    } else if (d_set_of_req && shared_blob_bytes && shared_blob_bytes <= kMaxTenantStageBytes) {
+        // multi-tenant batch: shared_blob_bytes = the largest ruleset blob of the batch;
+        // 4-wave workgroups, so more of them fall inside one AuthConfig's bucket
+        const uint32_t tblock = 256, tgrid = (n + tblock - 1) / tblock;
+        const uint32_t toff = (shared_blob_bytes + 15u) & ~15u;
+        hipLaunchKernelGGL(ajx_scan_fused_tenant, dim3(tgrid), dim3(tblock), toff + (tblock / 64) * kWinRingBytesPerWave,
+                           stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count,
+                           d_slow_ids, d_tri, d_err, d_bm, stride, toff, d_perm);
     } else {
         hipLaunchKernelGGL((ajx_scan_fused<false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
                            d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,

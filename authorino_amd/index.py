@@ -185,3 +185,14 @@ def select_sets(index: Index, hosts: Iterable[str], not_found: int = -1) -> np.n
             v = memo[h] = not_found if cfg is None else int(cfg)
         out[i] = v
     return out
+
+
+def bucket_order(sets: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    """The micro-batcher's bucketing of a multi-tenant batch: the permutation that groups
+    requests by AuthConfig (set id ascending) and, inside a bucket, by 8-byte document
+    length class, longest first. The first key lets a workgroup of the single-pass kernel
+    stage one ruleset in LDS; the second gives a wave's lanes similar token loads, as the
+    device length sort does for uniform batches (c4: 10.0 -> 7.7 ms per 2 M requests)."""
+    sets = np.asarray(sets, dtype=np.int64)
+    cls = np.asarray(lens, dtype=np.int64) >> 3
+    return np.lexsort((-cls, sets))

@@ -12,7 +12,8 @@ No dataset is fetched: everything is generated from numpy default_rng(seed).
       All(Any x4 of 8, All x4 of 8)
   c4  N docs x 10k multi-tenant AuthConfigs (8-32 patterns each, regex in 10 %), each
       request's AuthConfig selected on the host through the pkg/index restatement from a
-      Zipf(1.1) request host; requests bucketed by AuthConfig (set_of_req sorted)
+      Zipf(1.1) request host; requests bucketed by AuthConfig (set_of_req sorted), longest
+      first inside a bucket
   c5  N JWT-claims-heavy docs of 4096 +- 64 B, one AuthConfig with the full authz phase:
       4 top-level `when`, 4 authz configs (2 `when` + 16 rules each, 2 `matches`), 4
       response header selectors (2 plain, 2 json)
@@ -398,7 +399,7 @@ def make_c4(n: int, seed: int = 4, n_configs: int = 10000, n_wild: int = 100) ->
     host index (requests without one are dropped, as the reference answers NOT_FOUND
     before any evaluation); the batch is bucketed by AuthConfig. Document bodies are the
     c2 generator's (Authorization JSON of ~1 KiB)."""
-    from .index import select_sets
+    from .index import bucket_order, select_sets
 
     idx, exprs = c4_index_and_rules(n_configs, n_wild, seed=4)
     rng = np.random.default_rng(seed)
@@ -407,11 +408,11 @@ def make_c4(n: int, seed: int = 4, n_configs: int = 10000, n_wild: int = 100) ->
     sets = select_sets(idx, hosts)
     keep = np.nonzero(sets >= 0)[0][:n]
     sets = sets[keep]
-    order = np.argsort(sets, kind="stable")  # bucket by AuthConfig
     arena, offs, lens = make_docs(len(keep), seed)
+    order = bucket_order(sets, lens)  # bucket by AuthConfig, longest first inside a bucket
     return Workload("c4", arena, offs[order], lens[order], exprs[0],
                     f"{len(keep)} docs x {n_configs} AuthConfigs (8-32 patterns, regex in 10 %), "
-                    "host-index selection, bucketed by AuthConfig",
+                    "host-index selection, bucketed by AuthConfig and length class",
                     exprs=exprs, set_of_req=sets[order].astype(np.uint32),
                     hosts=[hosts[keep[i]] for i in order])
 

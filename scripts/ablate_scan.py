@@ -30,6 +30,7 @@ sor = torch.from_numpy(w.set_of_req.view(np.int32)).to(dev) if w.set_of_req is n
 L = runtime.load_library()
 L.authjx_debug_ablate.argtypes = [C.c_void_p, C.c_int]
 L.authjx_debug_len_sort.argtypes = [C.c_void_p, C.c_int]
+L.authjx_debug_tenant_stage.argtypes = [C.c_void_p, C.c_int]
 arena = torch.from_numpy(w.arena).to(dev)
 offs = torch.from_numpy(w.offs.view(np.int64)).to(dev)
 lens = torch.from_numpy(w.lens.view(np.int32)).to(dev)
@@ -45,7 +46,8 @@ outs = {}
 for rep in range(6):
     for mode in MODES:
         L.authjx_debug_ablate(ctx._h, mode % 100)
-        L.authjx_debug_len_sort(ctx._h, 2 if mode >= 200 else 0 if mode >= 100 else 1)
+        L.authjx_debug_len_sort(ctx._h, 2 if 200 <= mode < 300 else 0 if 100 <= mode < 200 else 1)
+        L.authjx_debug_tenant_stage(ctx._h, 0 if 300 <= mode < 400 else 1)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
         ctx.eval_device(rss, arena, offs, lens, tri, err, bm, set_of_req=sor, stream=stream.cuda_stream)

@@ -107,3 +107,15 @@ def test_c4_workload_selection_and_bucketing():
     assert w.n == 2000 and np.all(np.diff(w.set_of_req.astype(np.int64)) >= 0)
     assert all(8 <= len(e.flatten()[0]) <= 32 for e in w.exprs)
     assert sum(any(p.operator == 5 for p in e.flatten()[0]) for e in w.exprs) > 20
+
+
+def test_bucket_order_groups_by_config_then_longest_first():
+    rng = np.random.default_rng(5)
+    sets = rng.integers(0, 50, 5000)
+    lens = rng.integers(700, 1400, 5000)
+    o = ix.bucket_order(sets, lens)
+    assert np.array_equal(np.sort(o), np.arange(5000))
+    s, c = sets[o], lens[o] >> 3
+    assert (np.diff(s) >= 0).all()
+    same = np.diff(s) == 0
+    assert (np.diff(c)[same] <= 0).all()
