@@ -42,6 +42,10 @@ struct authjx_ctx {
     uint32_t perm_cap = 0;
     int len_sort = 1;            // order requests by length class before the single-pass kernel
     int no_tenant_stage = 0;     // profiling: multi-tenant batches read tables from global memory
+    // the capture rows in d_rows: written by the last single-ruleset, single-pass
+    // evaluation of rows_rs over rows_n requests (nullptr: none usable)
+    const authjx_ruleset* rows_rs = nullptr;
+    uint32_t rows_n = 0, rows_stride = 0;
     int force_scan = 0;
     int ablate = 0;  // profiling only: run a reduced stage A (1 loads, 2 loads+classify)
     float last_ms = 0.f;
@@ -251,6 +255,9 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         if (rc != AUTHJX_OK) return rc;
     }
     HIP_OK(hipEventRecord(ctx->ev0, s));
+    ctx->rows_rs = (!ctx->force_scan && n_sets == 1 && ctx->ablate == 0) ? sets[0] : nullptr;
+    ctx->rows_n = n;
+    ctx->rows_stride = row_stride;
     if (ctx->force_scan)
         HIP_OK(ajx::launch_eval_scan(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
@@ -300,6 +307,7 @@ int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* set
     int rc = ensure_sets(ctx, sets, n_sets, s);
     if (rc != AUTHJX_OK) return rc;
     const bool exact = ctx->force_scan != 0;  // the exact Get per selector (cross-check)
+    ctx->rows_rs = nullptr;  // (the rows are rewritten for this ruleset)
     if (!exact && (rc = ensure_work(ctx, n, row_stride, s)) != AUTHJX_OK) return rc;
     const uint32_t* perm = nullptr;
     if (!exact && ctx->len_sort && n_sets == 1 && n >= 4096) {
@@ -311,6 +319,25 @@ int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* set
     HIP_OK(ajx::launch_select(ctx->d_sets, d_set_of_req, shared_bytes, d_arena, d_offs, d_lens, n,
                               reinterpret_cast<uint32_t*>(d_out_values), values_stride,
                               exact ? nullptr : ctx->d_rows, row_stride, ctx->d_slow, ctx->d_slow + 1, perm, s));
+    return AUTHJX_OK;
+}
+
+int authjx_select_from_eval_device(authjx_ctx* ctx, const authjx_ruleset* rs, uint32_t first_pattern,
+                                   const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens,
+                                   uint32_t n, authjx_value* d_out_values, uint32_t values_stride, void* stream) {
+    if (!ctx || !rs || values_stride == 0 || (n && (!d_arena || !d_offs || !d_lens || !d_out_values)))
+        return AUTHJX_EINVAL;
+    if (first_pattern + values_stride > rs->c.n_patterns) return AUTHJX_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    // the rows must be the last evaluation's, of this ruleset, over this many requests
+    if (ctx->rows_rs != rs || ctx->rows_n != n) return AUTHJX_EINVAL;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    HIP_OK(hipSetDevice(ctx->device));
+    const authjx_ruleset* one[1] = {rs};
+    int rc = ensure_sets(ctx, one, 1, s);
+    if (rc != AUTHJX_OK) return rc;
+    HIP_OK(ajx::launch_select_rows(ctx->d_sets, d_arena, d_offs, d_lens, n, reinterpret_cast<uint32_t*>(d_out_values),
+                                   values_stride, ctx->d_rows, ctx->rows_stride, first_pattern, s));
     return AUTHJX_OK;
 }
 

@@ -526,7 +526,8 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
                                                          const uint64_t* __restrict__ offs,
                                                          const uint32_t* __restrict__ lens, uint32_t n,
                                                          uint32_t* __restrict__ out, uint32_t stride,
-                                                         const uint64_t* __restrict__ rows, uint32_t row_stride) {
+                                                         const uint64_t* __restrict__ rows, uint32_t row_stride,
+                                                         uint32_t p0) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     // the single-pass scan's capture row when it has one (not on the slow list)
@@ -540,9 +541,13 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
     const uint8_t* lits = blob + h->off_literals;
     const uint8_t* doc = arena + offs[r];
     const uint32_t len = lens[r];
-    const uint32_t np = h->n_patterns < stride ? h->n_patterns : stride;
-    for (uint32_t p = 0; p < np; p++) {
-        uint32_t* o = out + ((size_t)r * stride + p) * 3;
+    // patterns [p0, p0 + stride): the whole ruleset (p0 = 0) or, after a forest
+    // evaluation, the response selectors compiled as its last tree
+    const uint32_t avail = h->n_patterns > p0 ? h->n_patterns - p0 : 0u;
+    const uint32_t np = avail < stride ? avail : stride;
+    for (uint32_t q = 0; q < np; q++) {
+        const uint32_t p = p0 + q;
+        uint32_t* o = out + ((size_t)r * stride + q) * 3;
         if (pats[p].state == P_UNSUPPORTED) {
             o[0] = 0;
             o[1] = 0;
@@ -607,7 +612,18 @@ hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
     hipLaunchKernelGGL(ajx_select_values, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                       d_lens, n, d_out, stride, d_rows, row_stride);
+                       d_lens, n, d_out, stride, d_rows, row_stride, 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_rows(const uint8_t* const* d_sets, const uint8_t* d_arena, const uint64_t* d_offs,
+                              const uint32_t* d_lens, uint32_t n, uint32_t* d_out, uint32_t stride,
+                              const uint64_t* d_rows, uint32_t row_stride, uint32_t p0, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t block = 256;
+    const uint32_t grid = (n + block - 1) / block;
+    hipLaunchKernelGGL(ajx_select_values, dim3(grid), dim3(block), 0, stream, d_sets, nullptr, d_arena, d_offs,
+                       d_lens, n, d_out, stride, d_rows, row_stride, p0);
     return hipGetLastError();
 }
 

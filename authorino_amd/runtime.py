@@ -49,6 +49,7 @@ EXPORTS = [
     "authjx_ruleset_patterns", "authjx_ruleset_selectors", "authjx_pattern_error",
     "authjx_eval_batch_device", "authjx_eval_batch", "authjx_last_kernel_ms", "authjx_set_exact_scan",
     "authjx_last_exact_count", "authjx_select_batch_device", "authjx_select_batch", "authjx_compile_forest",
+    "authjx_select_from_eval_device",
     "authjx_ruleset_trees",
 ]
 
@@ -103,6 +104,10 @@ def load_library(path: str = LIB_PATH):
             C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
             C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
         L.authjx_select_batch_device.restype = C.c_int
+        L.authjx_select_from_eval_device.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+            C.c_uint32, C.c_void_p]
+        L.authjx_select_from_eval_device.restype = C.c_int
         L.authjx_select_batch.argtypes = [
             C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
             C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
@@ -147,9 +152,12 @@ class Context:
         pats, nodes, root = expr.flatten()
         return Ruleset(self, [(p.selector, int(p.operator), p.value) for p in pats], nodes, root)
 
-    def compile_forest(self, exprs) -> "Ruleset":
+    def compile_forest(self, exprs, extra_selectors=None) -> "Ruleset":
         """Several expressions (None = nil) as one ruleset (authjx_compile_forest): one
-        scan per document, one result per expression."""
+        scan per document, one result per expression. extra_selectors: gjson paths added
+        as a last, root-less tree of EQ "" patterns (its result is T), so that the same
+        scan captures them for select_from_eval_device at pattern index
+        n_patterns - len(extra_selectors)."""
         trees = []
         for e in exprs:
             if e is None:
@@ -157,6 +165,8 @@ class Context:
             else:
                 pats, nodes, root = e.flatten()
                 trees.append(([(p.selector, int(p.operator), p.value) for p in pats], nodes, root))
+        if extra_selectors:
+            trees.append(([(p, 1, "") for p in extra_selectors], [], -1))
         return Ruleset(self, None, None, None, forest=trees)
 
     def eval_device(self, sets: Sequence["Ruleset"], arena, offs, lens, out_tri, out_err=None, out_bm=None,
@@ -235,6 +245,17 @@ class Context:
             self._h, sarr, len(sets), ptr(set_of_req), ptr(arena), ptr(offs), ptr(lens), n, ptr(out),
             int(out.shape[1]), C.c_void_p(stream) if stream else None)
         _check(rc, "authjx_select_batch_device")
+
+    def select_from_eval_device(self, rs, first_pattern: int, arena, offs, lens, out, stream=None) -> None:
+        """authjx_select_from_eval_device: the values of patterns [first_pattern,
+        first_pattern + out.shape[1]) of `rs` from the capture rows of the last
+        eval_device(rs, ...) over the same tensors (no second document scan). Asynchronous."""
+        n = int(lens.numel())
+        ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+        rc = load_library().authjx_select_from_eval_device(
+            self._h, rs._h, int(first_pattern), ptr(arena), ptr(offs), ptr(lens), n, ptr(out), int(out.shape[1]),
+            C.c_void_p(stream) if stream else None)
+        _check(rc, "authjx_select_from_eval_device")
 
     def select_host_arena(self, sets, arena, offs, lens, set_of_req=None) -> np.ndarray:
         """gjson.Get of every pattern selector of each request's ruleset on the device

@@ -164,16 +164,18 @@ def main():
     ctx = runtime.Context(local)
     phase = w.auth_config is not None  # c5: the whole authorization phase per request
     if phase:
-        # one forest ruleset (top-level when, each evaluator's when and rules: one scan per
-        # document) + the response-header selectors (authjx_select_batch_device)
+        # one forest ruleset: top-level when, each evaluator's when and rules, and last the
+        # response-header selectors as a root-less tree; one scan per document captures
+        # them all, and authjx_select_from_eval_device reads the selectors' spans from it
         from authorino_amd.response import ResponseSelectors
 
         cfg = w.auth_config
         exprs = [cfg.conditions] + [e for c in cfg.authorization for e in (c.conditions, c.rules)]
-        rss = [ctx.compile_forest(exprs)]
         sel = ResponseSelectors(cfg.response, ctx)
-        R = rss[0].n_patterns
-        rpr = np.full(w.n, R, dtype=np.int64)
+        rss = [ctx.compile_forest(exprs, extra_selectors=sel.paths)]
+        R = rss[0].n_patterns  # (bitmap width: phase patterns + the selectors' entries)
+        r_phase = R - len(sel.paths)
+        rpr = np.full(w.n, r_phase, dtype=np.int64)
     else:
         rpr = w.patterns_per_request()  # R of each request's rule set
         R = int(max(len(e.flatten()[0]) for e in w.sets))
@@ -197,15 +199,16 @@ def main():
     def step():
         ctx.eval_device(rss, arena, offs, lens, tri, err, bm, set_of_req=sor, stream=sp)
         if phase:
-            ctx.select_device([sel.ruleset], arena, offs, lens, spans, stream=sp)
+            ctx.select_from_eval_device(rss[0], r_phase, arena, offs, lens, spans, stream=sp)
 
     elapsed, kern_ms = timed_steps(step, args.steps, args.warmup, dist, torch, dev, stream)
 
     total_req = w.n * args.steps * world
     value = int(rpr.sum()) * args.steps * world / elapsed  # shards are equal-sized (weak scaling)
     # doc read once + pattern bitmap + one result byte per tree (+ 12-B spans of the response
-    # selectors for c5)
-    algo_bytes = int(w.lens.astype(np.int64).sum()) + int(((rpr + 7) // 8 + nt).sum())
+    # selectors for c5; its selector tree's result byte is not counted)
+    nt_out = nt - 1 if phase else nt
+    algo_bytes = int(w.lens.astype(np.int64).sum()) + int(((rpr + 7) // 8 + nt_out).sum())
     if phase:
         algo_bytes += w.n * len(sel.paths) * 12
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
@@ -222,12 +225,12 @@ def main():
     extra = {}
     if phase:
         # the phase decision from the per-tree results (auth_pipeline.go:454-457, :287-322)
-        t = tri.cpu().numpy().reshape(w.n, nt)
+        t = tri.cpu().numpy().reshape(w.n, nt)[:, :nt_out]  # (the last tree: response selectors)
         skipped = t[:, 0] != runtime.T
         ok = np.ones(w.n, dtype=bool)
         for k in range(len(cfg.authorization)):
             ok &= (t[:, 1 + 2 * k] != runtime.T) | (t[:, 2 + 2 * k] == runtime.T)
-        extra = {"phase": {"trees": nt, "skipped": int(skipped.sum()), "allowed": int((skipped | ok).sum()),
+        extra = {"phase": {"trees": nt_out, "skipped": int(skipped.sum()), "allowed": int((skipped | ok).sum()),
                            "response_selectors": len(sel.paths)}}
         if rank == 0 and world == 1 and not args.no_cpu:
             cpu, parity = phase_cpu_baseline(w, exprs, args.cpu_seconds, t)
@@ -255,10 +258,10 @@ def main():
                 "workload": args.workload,
                 "description": w.description,
                 "requests_per_gpu": w.n,
-                "patterns": R if w.set_of_req is None else float(rpr.mean()),
+                "patterns": int(rpr.max()) if w.set_of_req is None else float(rpr.mean()),
                 "selectors": rss[0].n_selectors if len(rss) == 1 else float(np.mean([r.n_selectors for r in rss])),
                 "auth_configs": len(rss),
-                "trees_per_request": nt,
+                "trees_per_request": nt_out,
                 "doc_bytes_mean": float(w.lens.mean()),
                 "parallelism": f"dp{world} (independent request shards, no collective)",
             },

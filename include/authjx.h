@@ -194,6 +194,17 @@ int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* set
                                const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
                                const uint32_t* d_lens, uint32_t n, authjx_value* d_out_values,
                                uint32_t values_stride, void* stream);
+/* The values of patterns [first_pattern, first_pattern + values_stride) of `rs` from the
+ * capture rows the last authjx_eval_batch_device call on this context wrote: that call
+ * must have evaluated `rs` alone over the same d_arena / d_offs / d_lens (n requests),
+ * without authjx_set_exact_scan. For a phase compiled with authjx_compile_forest whose
+ * last tree holds the response selectors (AUTHJX_OP_EQ patterns, root -1), this resolves
+ * them without a second document scan: the gjson.Get of JSONValue.ResolveFor
+ * (pkg/json/json.go:41-53) after the rules of the same request. AUTHJX_EINVAL when the
+ * rows are not that evaluation's. Asynchronous on `stream`; order it after the eval. */
+int authjx_select_from_eval_device(authjx_ctx* ctx, const authjx_ruleset* rs, uint32_t first_pattern,
+                                   const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens,
+                                   uint32_t n, authjx_value* d_out_values, uint32_t values_stride, void* stream);
 /* Same from host buffers; synchronous. */
 int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
                         const uint32_t* set_of_req, const uint8_t* arena, uint64_t arena_len,

@@ -395,3 +395,52 @@ def test_forest_matches_single_rulesets(ctx):
             otri, oerr, _ = _oracle(e, w.arena, w.offs, w.lens)
             assert np.array_equal(tri, otri) and np.array_equal(err, oerr), k
     assert (ftri[:, -1] == 2).any()  # the static error decides some requests
+
+
+def test_select_from_eval_matches_select_batch(ctx):
+    """C5 response selectors compiled as the forest's last tree: their spans read from the
+    evaluation's capture rows equal authjx_select_batch_device's (its own scan), including
+    requests the single-pass kernel hands to the exact path; the phase trees' results do
+    not change; rows of another evaluation are refused."""
+    import torch
+
+    from authorino_amd import runtime, workloads
+    from authorino_amd.response import ResponseSelectors
+
+    w = workloads.make("c5", n=8192, seed=57)
+    cfg = w.auth_config
+    exprs = [cfg.conditions] + [e for c in cfg.authorization for e in (c.conditions, c.rules)]
+    sel = ResponseSelectors(cfg.response, ctx)
+    plain = ctx.compile_forest(exprs)
+    fused = ctx.compile_forest(exprs, extra_selectors=sel.paths)
+    k = len(sel.paths)
+    assert fused.n_patterns == plain.n_patterns + k and fused.n_trees == plain.n_trees + 1
+    arena = w.arena.copy()
+    cut = np.arange(0, w.n, 97)
+    arena[(w.offs[cut] + w.lens[cut] - 1).astype(np.int64)] = ord(" ")  # truncated: exact path
+    dev = torch.device("cuda", 0)
+    A = torch.from_numpy(arena).to(dev)
+    Of = torch.from_numpy(w.offs.view(np.int64)).to(dev)
+    Ln = torch.from_numpy(w.lens.view(np.int32)).to(dev)
+
+    def run(rs):
+        tri = torch.empty(w.n * rs.n_trees, dtype=torch.uint8, device=dev)
+        bm = torch.empty((w.n, (rs.n_patterns + 63) // 64), dtype=torch.int64, device=dev)
+        ctx.eval_device([rs], A, Of, Ln, tri, None, bm)
+        return tri
+
+    tri_f = run(fused)
+    got = torch.empty((w.n, k, 3), dtype=torch.int32, device=dev)
+    ctx.select_from_eval_device(fused, fused.n_patterns - k, A, Of, Ln, got)
+    torch.cuda.synchronize()
+    assert ctx.last_exact_count() >= len(cut)
+    want = torch.empty((w.n, k, 3), dtype=torch.int32, device=dev)
+    ctx.select_device([sel.ruleset], A, Of, Ln, want)
+    tri_p = run(plain)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), want.cpu().numpy())
+    tf = tri_f.cpu().numpy().reshape(w.n, fused.n_trees)
+    assert np.array_equal(tf[:, :plain.n_trees], tri_p.cpu().numpy().reshape(w.n, plain.n_trees))
+    assert (tf[:, -1] == runtime.T).all()
+    with pytest.raises(runtime.AuthjxError):  # the rows are the plain forest's now
+        ctx.select_from_eval_device(fused, fused.n_patterns - k, A, Of, Ln, got)
