@@ -158,7 +158,7 @@ struct RulesetHdr {
     uint32_t off_literals;
     uint32_t lit_bytes;
     uint32_t n_components;
-    uint32_t flags;  // bit0: has regex; bit1: has unsupported pattern; bit2: fast path ok; bit3: line engine ok
+    uint32_t flags;  // bit0: has regex; bit1: has unsupported pattern; bit2: fast path ok
     uint32_t n_trie_nodes;
     uint32_t off_trie_nodes;
     uint32_t off_trie_children;
@@ -172,7 +172,5 @@ struct RulesetHdr {
     uint64_t unsupported[2];    // pattern p can not be decided on the device
 };
 constexpr uint32_t kFlagFastOk = 4;
-constexpr uint32_t kFlagLinesOk = 8;   // eligible for the line engine (ajx_lines.h)
-constexpr uint32_t kLinesMaxDepth = 8; // selector depth the line engine tracks
 
 }  // namespace ajx

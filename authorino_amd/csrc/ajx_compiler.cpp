@@ -364,11 +364,6 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         if (nt && i < 128) null_true[i >> 6] |= bit;
     }
     if (fast_ok) flags |= kFlagFastOk;
-    // the line engine tracks live containers up to kLinesMaxDepth levels deep
-    bool lines_ok = fast_ok;
-    for (size_t s = 0; s < sels.size(); s++)
-        if (sels[s].comp_count > kLinesMaxDepth) lines_ok = false;
-    if (lines_ok) flags |= kFlagLinesOk;
 
     // ---- assemble ----
     Builder b;

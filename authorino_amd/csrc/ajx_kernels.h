@@ -37,10 +37,9 @@ constexpr uint32_t kMaxTenantStageBytes = 8 * 1024;
 // single-pass kernel + exact scan of the requests it hands over (d_slow_count is zeroed
 // on the stream first; d_slow_ids needs room for n entries). shared_blob_bytes: the
 // blob size of sets[0] when every request uses it and it fits kMaxSharedBlobBytes,
-// else 0. mode: 0 the single-pass kernel (default, ajx_fast.h); 5 the line engine
-// (ajx_lines.h, LDS ring); profiling only: 1 stage-A loads only, 2 stage-A loads +
-// classification, 3 stage A and stage B as separate launches, 11/12/13 line-engine
-// ablations.
+// else 0. mode: 0 the single-pass kernel (default, ajx_fast.h); profiling only: 1
+// stage-A loads only, 2 stage-A loads + classification, 3 stage A and stage B as
+// separate launches.
 hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,

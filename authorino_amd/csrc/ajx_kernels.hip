@@ -6,9 +6,6 @@
 //                Requests it can not prove gjson-equivalent go to a slow list.
 // ajx_patterns   stage B, one work-item per request: patterns on the captured values,
 //                T bitmap, And/Or fold.
-// ajx_scan_lines the line engine (ajx_lines.h), one work-item per request: the document
-//                in 128-B lines through a per-lane two-line LDS ring, one token loop
-//                per line, values evaluated from the ring; the default fast path.
 // ajx_eval_scan  one work-item per request on the slow list (or on every request when
 //                forced): for each selector an exact gjson.Get scan (ajx_device.h gj_get),
 //                then the patterns and the fold. Exact for arbitrary input bytes.
@@ -16,7 +13,6 @@
 
 #include "ajx_fast.h"
 #include "ajx_kernels.h"
-#include "ajx_lines.h"
 
 namespace ajx {
 
@@ -318,109 +314,6 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     }
 }
 
-// The line engine. Dynamic LDS: [blob copy (SHARED)] [ring: 4 waves x 16 KiB]. Every
-// thread reaches the staging barrier before any exits.
-constexpr uint32_t kLinesBlock = 256;
-#ifndef AJX_LINES_WAVES
-#define AJX_LINES_WAVES 2  // waves per SIMD the register budget is set for
-#endif
-constexpr uint32_t kRingBytesPerWave = 2 * kLine * 64;
-
-template <bool SHARED>
-__global__ __launch_bounds__(kLinesBlock, AJX_LINES_WAVES) void ajx_scan_lines(
-    const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
-    uint32_t n, uint64_t* __restrict__ rows, uint32_t row_stride, uint32_t* __restrict__ slow_count,
-    uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-    uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t ring_off, int ablate) {
-    extern __shared__ uint4 s_dyn[];
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint8_t* blob;
-    if constexpr (SHARED) {
-        const uint8_t* g = sets[0];
-        const uint32_t nq = reinterpret_cast<const RulesetHdr*>(g)->total_bytes / 16;
-        const uint4* g4 = reinterpret_cast<const uint4*>(g);
-        for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) s_dyn[i] = g4[i];
-        __syncthreads();
-        blob = reinterpret_cast<const uint8_t*>(s_dyn);
-    } else {
-        blob = sets[(set_of_req && r < n) ? set_of_req[r] : 0];
-    }
-    if (r >= n) return;
-    const uint8_t* d = arena + offs[r];
-    const uint32_t len = lens[r];
-    uint64_t* row = rows + (size_t)r * row_stride;
-    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    if (!(h->flags & kFlagLinesOk) || len >= (1u << 23)) {
-        row[0] = kRowSlow;
-        slow_ids[atomicAdd(slow_count, 1u)] = r;
-        return;
-    }
-    const uint32_t mis = (uint32_t)((uintptr_t)d & (kLine - 1));
-    LineScan sc;
-    sc.init(blob, d, len, mis);
-    sc.ring.base = reinterpret_cast<uint8_t*>(s_dyn) + ring_off + (threadIdx.x >> 6) * kRingBytesPerWave;
-    sc.ring.lane16 = (threadIdx.x & 63u) * 16u;
-    sc.ring.cstride = 64u * 16u;
-    // every 16-B chunk of a line that holds a document byte is inside that byte's page
-    const uint4* a4 = reinterpret_cast<const uint4*>(d - mis);
-    const uint32_t nlines = (mis + len + kLine - 1) / kLine;
-    Block16 R[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const uint4 v = a4[j];
-        R[j] = Block16{v.x, v.y, v.z, v.w};
-    }
-    uint32_t sink = 0;
-    for (uint32_t l = 0; l < nlines; l++) {
-        sc.line = l;
-        sc.ring.put_line(l, R);
-        if (ablate == 1) {  // profiling: loads + ring writes only
-            sink ^= R[0].x ^ R[7].w;
-            if (l + 1 < nlines)
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const uint4 v = a4[(l + 1) * 8 + j];
-                    R[j] = Block16{v.x, v.y, v.z, v.w};
-                }
-            continue;
-        }
-        sc.classify(R);
-        if (ablate == 2) sc.tk_lo = sc.tk_hi = 0;  // profiling: + classification
-        // (the next line is loaded after the token loop: its 32 registers are not held
-        // across the loop, which keeps the kernel at more waves per SIMD; the other
-        // waves cover the load)
-        sc.token_loop();
-        sc.flush();
-        if (sc.st >= X_DONE) break;
-        if (l + 1 < nlines) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint4 v = a4[(l + 1) * 8 + j];
-                R[j] = Block16{v.x, v.y, v.z, v.w};
-            }
-        }
-    }
-    if (ablate == 1 || ablate == 2) {
-        out_tri[r] = (uint8_t)(sink ^ (uint32_t)sc.tk_lo ^ sc.st);
-        return;
-    }
-    uint64_t t[2], u[2] = {h->unsupported[0], h->unsupported[1]};
-    if (!sc.finish(&t[0], &t[1])) {
-        row[0] = kRowSlow;
-        slow_ids[atomicAdd(slow_count, 1u)] = r;
-        return;
-    }
-    if (out_bm) {
-        uint64_t* orow = out_bm + (size_t)r * stride;
-        orow[0] = t[0];
-        if (stride > 1) orow[1] = t[1];
-        for (uint32_t w = 2; w < stride; w++) orow[w] = 0ull;
-    }
-    const uint64_t se[2] = {h->static_error[0], h->static_error[1]};
-    fold_outputs(r, blob, h, t, u, se, out_tri, out_err);
-}
-
 // ---------------------------------------------------------------------------------
 // Length bucketing: a wave of the single-pass kernel runs each window's token loop as
 // long as its busiest lane, and the whole document loop as long as its longest
@@ -683,30 +576,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                                d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off, nullptr);
         return hipGetLastError();
     }
-    if (mode == 5 || mode >= 10) {  // the line engine; 11/12/13 profiling ablations
-        const int lines_ablate = mode >= 10 ? mode - 10 : 0;
-        const uint32_t lgrid = (n + kLinesBlock - 1) / kLinesBlock;
-        const uint32_t dyn = ring_off + (kLinesBlock / 64) * kRingBytesPerWave;
-        static bool attr_set[2] = {false, false};
-        if (!attr_set[shared]) {
-            if (shared)
-                e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ajx_scan_lines<true>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            else
-                e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ajx_scan_lines<false>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (e != hipSuccess) return e;
-            attr_set[shared] = true;
-        }
-        if (shared)
-            hipLaunchKernelGGL((ajx_scan_lines<true>), dim3(lgrid), dim3(kLinesBlock), dyn, stream, d_sets,
-                               d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids,
-                               d_tri, d_err, d_bm, stride, ring_off, lines_ablate);
-        else
-            hipLaunchKernelGGL((ajx_scan_lines<false>), dim3(lgrid), dim3(kLinesBlock), dyn, stream, d_sets,
-                               d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids,
-                               d_tri, d_err, d_bm, stride, ring_off, lines_ablate);
-    } else if (mode == 3) {  // profiling split: stage A and stage B as two launches
+    if (mode == 3) {  // profiling split: stage A and stage B as two launches
         if (shared) {
             hipLaunchKernelGGL((ajx_scan_fast<0, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off, nullptr);

@@ -154,18 +154,3 @@ def eval_fast(hr: "HostRuleset", doc, mis: int = 0):
     err = C.c_int32(-1)
     t = L.ht_eval_fast(hr._h, d, len(d), mis, res, C.byref(err))
     return t, err.value, list(res)[: hr.n]
-
-
-def eval_lines(hr: "HostRuleset", doc, mis: int = 0, fill: int = 0x41):
-    """Line engine on the host: (tri | -1 exact scan | -2 not eligible, err, res)."""
-    L = lib()
-    if not hasattr(L, "_lines_declared"):
-        L.ht_eval_lines.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint8,
-                                    C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
-        L.ht_eval_lines.restype = C.c_int
-        L._lines_declared = True
-    d = _b(doc)
-    res = (C.c_uint8 * max(hr.n, 1))()
-    err = C.c_int32(-1)
-    t = L.ht_eval_lines(hr._h, d, len(d), mis, fill, res, C.byref(err))
-    return t, err.value, list(res)[: hr.n]

@@ -122,3 +122,38 @@ def dump_ws(v, rng):
 def rand_doc_ws(rng):
     v = ("o", [(KEYS[rng.integers(0, len(KEYS))], rand_value(rng, 4)) for _ in range(int(rng.integers(1, 7)))])
     return (_ws(rng) + dump_ws(v, rng) + _ws(rng)).encode("utf-8")
+
+
+def chain(n):
+    nodes = [(0, -1, -1, i) for i in range(n)]
+    root = -1
+    for i in reversed(range(n)):
+        nodes.append((1, i, root, -1))
+        root = len(nodes) - 1
+    return nodes, root
+
+
+def long_doc(rng, pats):
+    """A compact document whose selector values are long strings / arrays, placed after
+    padding so that they straddle line boundaries."""
+    parts = []
+    for k in range(int(rng.integers(1, 6))):
+        parts.append('"pad%d":"%s"' % (k, "p" * int(rng.integers(0, 300))))
+    for sel, op, val in pats:
+        keys = sel.split(".")
+        if any(not k or "\\" in k or '"' in k for k in keys):
+            continue
+        v = rng.random()
+        if v < 0.3:
+            inner = json.dumps(val) if rng.random() < 0.5 else '"%s"' % ("L" * int(rng.integers(100, 300)))
+        elif v < 0.6:
+            inner = "[" + ",".join('"%s"' % ("e" * int(rng.integers(0, 150))) for _ in range(int(rng.integers(0, 6)))) + "]"
+        elif v < 0.8:
+            inner = "[" + ",".join(['{"k":"%s"}' % ("o" * int(rng.integers(0, 90))), "12", "true", "null", json.dumps(val)]) + "]"
+        else:
+            inner = str(int(rng.integers(-10**12, 10**12)))
+        for k in reversed(keys):
+            inner = "{%s:%s}" % (json.dumps(k, ensure_ascii=False), inner)
+        parts.append(inner[1:-1])
+    rng.shuffle(parts)
+    return ("{" + ",".join(parts) + "}").encode()

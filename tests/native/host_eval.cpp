@@ -8,7 +8,6 @@
 
 #include "../../authorino_amd/csrc/ajx_compiler.h"
 #include "../../authorino_amd/csrc/ajx_fast.h"
-#include "../../authorino_amd/csrc/ajx_lines.h"
 #include "../../authorino_amd/csrc/ajx_regex.h"
 
 using namespace ajx;
@@ -158,50 +157,4 @@ int ht_eval_fast(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_
 }
 }
 
-extern "C" {
-// line engine (ajx_lines.h), one lane: returns -1 when the document is handed to the
-// exact scan, else the tri-state; res[p] receives each pattern's value. `mis` (0..127)
-// places the copy at that offset within its first 128-B line. Bytes around the
-// document in its lines are filled with `fill` (the device reads neighbours there).
-int ht_eval_lines(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t fill, uint8_t* res, int32_t* err) {
-    const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
-    const RulesetHdr* hd = (const RulesetHdr*)blob;
-    if (!(hd->flags & kFlagLinesOk)) return -2;
-    mis &= 127;
-    std::vector<uint8_t> buf(len + 512, fill);
-    uintptr_t base = ((uintptr_t)buf.data() + 127) & ~(uintptr_t)127;
-    uint8_t* d = (uint8_t*)base + mis;
-    std::memcpy(d, doc, len);
-    alignas(16) uint8_t ring[256];
-    std::memset(ring, 0xA5, sizeof ring);
-    LineScan sc;
-    sc.init(blob, d, len, mis);
-    sc.ring.base = ring;
-    sc.ring.lane16 = 0;
-    sc.ring.cstride = 16;
-    const uint32_t nlines = (mis + len + 127) / 128;
-    const Block16* a = (const Block16*)(d - mis);
-    for (uint32_t l = 0; l < nlines && sc.st < X_DONE; l++) {
-        Block16 r[8];
-        for (int j = 0; j < 8; j++) r[j] = a[l * 8 + j];
-        sc.line = l;
-        sc.ring.put_line(l, r);
-        sc.run_line(r);
-    }
-    uint64_t t[2], u[2] = {hd->unsupported[0], hd->unsupported[1]};
-    if (!sc.finish(&t[0], &t[1])) return -1;
-    const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
-    for (uint32_t p = 0; p < hd->n_patterns; p++) {
-        uint64_t bit = 1ull << (p & 63);
-        uint32_t k = p >> 6;
-        res[p] = (hd->static_error[k] & bit) ? V_E : (u[k] & bit) ? V_U : (t[k] & bit) ? V_T : V_F;
-    }
-    const uint64_t se[2] = {hd->static_error[0], hd->static_error[1]};
-    int32_t ep2;
-    const uint8_t tri2 = run_fold_bits(code, hd->n_code, t, u, se, &ep2);
-    const uint8_t tri = run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
-    if (tri != tri2 || *err != ep2) return -3;  // the device fold disagrees with the reference fold
-    return tri;
-}
-}
 extern "C" uint32_t ht_blob_size(void* h) { return (uint32_t)((HtRuleset*)h)->c.blob.size(); }

@@ -73,8 +73,6 @@ def test_fuzz_fast_whitespace_runs(seed):
 def test_fast_long_values_across_windows(seed):
     """Long keys / values / arrays placed at random offsets so that tokens, key tails and
     scalars straddle the single-pass scanner's 64-byte windows."""
-    from test_fuzz_lines import _chain, _long_doc
-
     rng = np.random.default_rng(300 + seed)
     n_fast = n_all = 0
     for _ in range(60):
@@ -83,7 +81,7 @@ def test_fast_long_values_across_windows(seed):
         rs = O.Ruleset(pats, nodes, root)
         hr = H.HostRuleset(pats, nodes, root)
         for _ in range(10):
-            d = _long_doc(rng, pats)
+            d = FU.long_doc(rng, pats)
             ot = [rs.pattern(p, d) for p in range(len(pats))]
             if O.UNSUPPORTED in ot:
                 continue

@@ -204,52 +204,6 @@ def test_random_documents_and_selectors(ctx):
     assert checked > 5000
 
 
-@pytest.mark.parametrize("workload,n", [("c2", 30000), ("c3", 20000)])
-def test_line_engine_matches_oracle(ctx, workload, n):
-    """The alternative lane-per-request line engine (kernel mode 5, ajx_lines.h) against
-    the oracle on the workload documents and on random / malformed documents."""
-    import fuzz_util as FU
-    from authorino_amd import workloads as W
-
-    w = W.make(workload, n=n, seed=31)
-    rs = ctx.compile_expression(w.expr)
-    ctx.set_kernel_mode(5)
-    try:
-        tri, err, bm = ctx.eval_host_arena([rs], w.arena, w.offs, w.lens)
-        n_exact = ctx.last_exact_count()
-        rng = np.random.default_rng(9)
-        fuzz = []
-        for _ in range(10):
-            pats = FU.rand_patterns(rng, int(rng.integers(1, 8)))
-            nodes = [(0, -1, -1, i) for i in range(len(pats))]
-            root = -1
-            for i in reversed(range(len(pats))):
-                nodes.append((1, i, root, -1))
-                root = len(nodes) - 1
-            ors = O.Ruleset(pats, nodes, root)
-            docs = [FU.rand_doc(rng, ws=False) for _ in range(300)]
-            docs = [FU.mutate(rng, d) if rng.random() < 0.3 else d for d in docs]
-            if any(ors.pattern(p, docs[0]) == O.UNSUPPORTED for p in range(len(pats))):
-                continue
-            fuzz.append((ors, docs, ctx.eval_host([ctx.compile(pats, nodes, root)], docs)))
-    finally:
-        ctx.set_kernel_mode(0)
-    otri, oerr, obm = _oracle(w.expr, w.arena, w.offs, w.lens)
-    assert np.array_equal(tri, otri)
-    assert np.array_equal(err, oerr)
-    assert np.array_equal(bm, obm)
-    assert n_exact == 0  # every workload document took the line engine
-    for ors, docs, (ftri, ferr, fbm) in fuzz:
-        lens = np.array([len(d) for d in docs], dtype=np.uint32)
-        offs = np.zeros(len(docs), dtype=np.uint64)
-        offs[1:] = np.cumsum(lens[:-1])
-        arena = np.frombuffer(b"".join(docs) + b"\0", dtype=np.uint8)
-        gtri, gerr, gbm = O.eval_batch([ors], arena, offs, lens)
-        dec = ftri != 3
-        assert np.array_equal(ftri[dec], gtri[dec])
-        assert np.array_equal(fbm[dec], gbm[dec])
-
-
 def test_pipeline_batch_on_device():
     """The batched `when` + authorization phase (authorino_amd.pipeline) on the device
     against the same phase evaluated with the oracle (tests/test_pipeline_host.py)."""
