@@ -205,10 +205,29 @@ def _make_doc_c5(rng: np.random.Generator, target_len: int, uid: int) -> bytes:
     return s.encode("utf-8")
 
 
+def _volatile_spans(doc: bytes):
+    """Byte spans of a document whose contents no pattern depends on (bearer-token hex,
+    x-padding, the start of a c5 JWT): (start, length, alphabet) with at most 32 bytes
+    each, rewritten per copy so that tiled documents are all distinct."""
+    import re
+
+    out = []
+    for m in re.finditer(rb"Bearer (?:eyJ)?([0-9a-zA-Z_-]{8,})", doc):
+        out.append((m.start(1), min(32, m.end(1) - m.start(1)), 0))
+    for m in re.finditer(rb'"x-padding":"(p{8,})"', doc):
+        out.append((m.start(1), min(32, m.end(1) - m.start(1)), 1))
+    return out
+
+
+_ALPHABETS = [np.frombuffer(b"0123456789abcdef", dtype=np.uint8), np.frombuffer(b"pqrstuvwxyz", dtype=np.uint8)]
+
+
 def make_docs(n: int, seed: int, lo: int = 768, hi: int = 1280, unique: int = 4096,
-              maker=None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+              maker=None, uniquify: bool = False) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     """n documents (lengths ~U[lo, hi]) packed into (arena, offs, lens). `unique` distinct
-    documents are generated and tiled by a random permutation."""
+    documents are generated and tiled by a random permutation; with `uniquify` every copy
+    also gets its own random bearer-token / padding bytes (same length and structure, no
+    pattern reads them), so no two documents of the batch are byte-identical."""
     rng = np.random.default_rng(seed)
     m = min(n, unique)
     maker = maker or _make_doc
@@ -220,6 +239,24 @@ def make_docs(n: int, seed: int, lo: int = 768, hi: int = 1280, unique: int = 40
     if n:
         offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
     arena = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    if uniquify and n > m:
+        spans = [_volatile_spans(b) for b in base]
+        for alpha_id, alpha in enumerate(_ALPHABETS):
+            # (template, start, length) of this alphabet's spans, then every copy's bytes
+            tmpl = [(t, st, ln) for t, sp in enumerate(spans) for st, ln, a in sp if a == alpha_id]
+            if not tmpl:
+                continue
+            per = {}
+            for t, st, ln in tmpl:
+                per.setdefault(t, []).append((st, ln))
+            rel = [np.concatenate([np.arange(st, st + ln) for st, ln in per.get(t, [])]).astype(np.int64)
+                   if t in per else np.zeros(0, dtype=np.int64) for t in range(m)]
+            cnt = np.array([len(r) for r in rel], dtype=np.int64)[idx]
+            step = 1 << 16  # copies per chunk (bounded index arrays)
+            for c0 in range(0, n, step):
+                ii = np.arange(c0, min(n, c0 + step))
+                pos = np.concatenate([rel[idx[i]] for i in ii]) + np.repeat(offs[ii].astype(np.int64), cnt[ii])
+                arena[pos] = alpha[rng.integers(0, len(alpha), size=len(pos))]
     return arena, offs, lens
 
 
@@ -394,7 +431,8 @@ def c4_hosts(n: int, n_configs: int, n_wild: int, rng: np.random.Generator) -> L
     return hosts
 
 
-def make_c4(n: int, seed: int = 4, n_configs: int = 10000, n_wild: int = 100) -> Workload:
+def make_c4(n: int, seed: int = 4, n_configs: int = 10000, n_wild: int = 100, unique: int = 4096,
+            uniquify: bool = False) -> Workload:
     """C4: multi-tenant batch. Each request's AuthConfig comes from the
     host index (requests without one are dropped, as the reference answers NOT_FOUND
     before any evaluation); the batch is bucketed by AuthConfig. Document bodies are the
@@ -408,7 +446,7 @@ def make_c4(n: int, seed: int = 4, n_configs: int = 10000, n_wild: int = 100) ->
     sets = select_sets(idx, hosts)
     keep = np.nonzero(sets >= 0)[0][:n]
     sets = sets[keep]
-    arena, offs, lens = make_docs(len(keep), seed)
+    arena, offs, lens = make_docs(len(keep), seed, unique=unique, uniquify=uniquify)
     order = bucket_order(sets, lens)  # bucket by AuthConfig, longest first inside a bucket
     return Workload("c4", arena, offs[order], lens[order], exprs[0],
                     f"{len(keep)} docs x {n_configs} AuthConfigs (8-32 patterns, regex in 10 %), "
@@ -463,26 +501,36 @@ def c5_auth_config():
     return AuthConfig(conditions=top, authorization=authz, response=resp)
 
 
-def make(name: str, n: Optional[int] = None, seed: Optional[int] = None) -> Workload:
+DEFAULT_SEEDS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5}
+
+
+def make(name: str, n: Optional[int] = None, seed: Optional[int] = None, unique: Optional[int] = None,
+         uniquify: bool = False) -> Workload:
+    """A BASELINE config's workload. unique / uniquify: see make_docs (the bench uses
+    16384 templates for c2/c3/c4 and distinct bytes in every copy)."""
     name = name.lower()
+    seed = seed if seed is not None else DEFAULT_SEEDS.get(name, 0)
+    kw = {"uniquify": uniquify}
+    if unique is not None:
+        kw["unique"] = unique
     if name == "c1":
-        arena, offs, lens = make_docs(1, seed if seed is not None else 1, 680, 720)
+        arena, offs, lens = make_docs(1, seed, 680, 720)
         return Workload("c1", arena, offs, lens, c1_expression(), "1 doc x All(eq, incl, matches)")
     if name == "c2":
         n = n if n is not None else 1 << 20
-        arena, offs, lens = make_docs(n, seed if seed is not None else 2)
+        arena, offs, lens = make_docs(n, seed, **kw)
         return Workload("c2", arena, offs, lens, c2_expression(),
                         f"{n} docs (768-1280 B) x All of 16 eq/neq/incl over 12 selectors")
     if name == "c3":
         n = n if n is not None else 1 << 20
-        arena, offs, lens = make_docs(n, seed if seed is not None else 3)
+        arena, offs, lens = make_docs(n, seed, **kw)
         return Workload("c3", arena, offs, lens, c3_expression(),
                         f"{n} docs x 64 patterns (24 eq/12 neq/10 incl/10 excl/8 matches), All(Any x4, All x4)")
     if name == "c4":
-        return make_c4(n if n is not None else 1 << 21, seed if seed is not None else 4)
+        return make_c4(n if n is not None else 1 << 21, seed, **kw)
     if name == "c5":
         n = n if n is not None else 1 << 21
-        arena, offs, lens = make_docs(n, seed if seed is not None else 5, 4032, 4160, maker=_make_doc_c5)
+        arena, offs, lens = make_docs(n, seed, 4032, 4160, maker=_make_doc_c5, **kw)
         cfg = c5_auth_config()
         return Workload("c5", arena, offs, lens, cfg.authorization[0].rules,
                         f"{n} docs of 4096+-64 B x full authz phase (4 when, 4 authz x (2 when + 16 rules), "

@@ -1,20 +1,25 @@
 """bench.py — headline benchmark (BASELINE.json metric) for the pattern-matching hot path.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4] [--n N_REQUESTS]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5] [--requests N]
 
 A step = one pass of the hot path (ajx kernels behind authjx_eval_batch_device) over one
 batch of N synthetic Authorization-JSON documents already resident in HBM. N=1 runs the
 config BASELINE.json's metric is quoted on that fits one GPU (configs[1], "c2": 1M
-requests x 16 eq/neq/incl patterns). Multi-GPU: one process per GPU
-(torch.distributed.run), each rank evaluates its own shard (weak scaling, no data-path
-collective); the timed region is bracketed by barrier + synchronize, the max over ranks
-is reported. Rank 0 prints one JSON line. c4 (multi-tenant: 10k AuthConfigs, per-request
-set ids from the host index) defaults to 2M requests per GPU (16M over 8 GPUs).
+requests x 16 eq/neq/incl patterns). Multi-GPU: one process per GPU, each rank
+evaluating its own shard (weak scaling, no data-path collective); `--gpus N` started
+without a torch.distributed.run environment re-launches itself under
+torch.distributed.run (before touching any GPU) with N ranks. The timed region is
+bracketed by barrier + synchronize, the max over ranks is reported, rank 0 prints one
+JSON line. c4 (10k AuthConfigs, per-request set ids from the host index) and c5 (full
+phase, 4 KiB documents) default to 2M requests per GPU (16M over 8 GPUs).
+`--dry-run` runs the same distributed driver on the CPU (gloo) with a stand-in step, for
+the CPU tests of the N>1 path.
 """
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,11 +37,49 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2")
-    ap.add_argument("--n", type=int, default=None, help="requests per GPU per step (c2/c3 1M, c4 2M)")
+    ap.add_argument("--requests", "--n", dest="n", type=int, default=None,
+                    help="requests per GPU per step (c2/c3 1M, c4/c5 2M)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
+    ap.add_argument("--unique", type=int, default=None,
+                    help="distinct document templates (default 16384 for c2/c3/c4, 4096 for c5)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo test of the distributed driver: no GPU, a stand-in step")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relaunch(args) -> None:
+    """`--gpus N` (N > 1) outside a torch.distributed.run environment: start N ranks as a
+    child torch.distributed.run and exit with its status. Runs before anything touches
+    the GPU (the child is a separate process, never an exec)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    # (`--n` would be an ambiguous abbreviation of torch.distributed.run's own options)
+    cmd += ["--requests" if a == "--n" else a for a in sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def host_threads() -> int:
+    """Host threads the CPU baseline uses: every core this process may run on, capped by
+    OMP_NUM_THREADS (the GPU box sets it to its per-GPU CPU share)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
 
 
 def cpu_baseline(w, rpr, target_s, gpu_tri, gpu_bm):
@@ -45,8 +88,7 @@ def cpu_baseline(w, rpr, target_s, gpu_tri, gpu_bm):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    threads = host_threads()
     rss = [pyoracle.Ruleset.from_expression(e) for e in w.sets]
     sor = w.set_of_req
     pilot = min(w.n, 16384)
@@ -74,7 +116,8 @@ def cpu_baseline(w, rpr, target_s, gpu_tri, gpu_bm):
         "cores": threads,
         "kind": "port",
         "sample": f"first {sample} of the {w.n} synthetic docs x {reps} passes, same ruleset, oracle/ C "
-                  f"restatement (gjson re-scan per pattern like the reference), {threads} host threads, {dt:.1f}s",
+                  f"restatement (gjson re-scan per pattern like the reference, each pattern evaluated once), "
+                  f"{threads} host threads, {dt:.1f}s",
     }, {"sample": sample, "mismatches": mism}
 
 
@@ -84,8 +127,7 @@ def phase_cpu_baseline(w, exprs, target_s, gpu_tri):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    threads = host_threads()
     rss = [pyoracle.Ruleset.from_expression(e) for e in exprs]
     R = sum(len(e.flatten()[0]) for e in exprs)
     k = min(w.n, 4096)
@@ -141,14 +183,78 @@ def timed_steps(step, steps, warmup, dist, torch, dev, stream=None):
     return elapsed, kern_ms
 
 
+def c1_cpu_ns_per_op(reps: int = 200000) -> dict:
+    """BASELINE configs[0]: one ~700-byte document, All(eq, incl,
+    matches), the oracle on ONE host thread, ns per Matches call (the analogue of the
+    reference's BenchmarkJSONPatternMatchingAuthz, pkg/evaluators/authorization/json_test.go:275-303)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from authorino_amd import workloads
+
+    w = workloads.make("c1")
+    rs = pyoracle.Ruleset.from_expression(w.expr)
+    offs = np.zeros(reps, dtype=np.uint64)  # the same document, reps times
+    lens = np.full(reps, int(w.lens[0]), dtype=np.uint32)
+    pyoracle.eval_batch([rs], w.arena, offs[:1000], lens[:1000], nthreads=1)
+    t0 = time.perf_counter()
+    tri, _, _ = pyoracle.eval_batch([rs], w.arena, offs, lens, nthreads=1)
+    dt = time.perf_counter() - t0
+    return {"ns_per_op": dt / reps * 1e9, "patterns": 3, "doc_bytes": int(w.lens[0]), "threads": 1,
+            "result": int(tri[0]), "kind": "port",
+            "note": "oracle/ C restatement (gjson re-scan per pattern, DFA regex), not the Go binary; "
+                    "the published Go figure is 1.797 us/op for 2 eq patterns on a Xeon 8370C core"}
+
+
+def dry_main(args, world, rank, dist, torch) -> None:
+    """The distributed driver without a GPU (gloo): same sharding, seeds, barriers, timing
+    and JSON line; the step is a stand-in (a checksum over the rank's shard)."""
+    from authorino_amd import workloads
+
+    seed = workloads.DEFAULT_SEEDS.get(args.workload, 0) + 7919 * rank
+    w = workloads.make(args.workload, n=args.n or 256, seed=seed, unique=args.unique or 64, uniquify=True)
+    acc = [0]
+
+    def step():
+        acc[0] += int(w.arena.sum(dtype=np.uint64)) + int(w.lens.sum())
+
+    elapsed, _ = timed_steps(step, args.steps, args.warmup, dist, torch, None)
+    shard = {"rank": rank, "seed": seed, "n": w.n, "first_doc_sha": __import__("hashlib").sha1(w.doc(0)).hexdigest()}
+    shards = [None] * world
+    if dist:
+        dist.all_gather_object(shards, shard)
+    else:
+        shards = [shard]
+    if rank == 0:
+        print(json.dumps({"metric": "request×rule evals/sec (dry run: stand-in step, no GPU)", "value": None,
+                          "unit": "request×rule evals/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                          "data": "synthetic", "dry_run": True, "shards": shards,
+                          "config": {"workload": args.workload, "requests_per_gpu": w.n,
+                                     "parallelism": f"dp{world} (independent request shards, no collective)"}}),
+              flush=True)
+
+
 def main():
     args = parse()
+    relaunch(args)  # --gpus N without torch.distributed.run: N child ranks, then exit
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != max(1, args.gpus) and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE", file=sys.stderr)
     dist = None
+    if args.dry_run:
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.init_process_group("gloo")
+        dry_main(args, world, rank, dist, torch)
+        if dist:
+            dist.destroy_process_group()
+        return
     if world > 1:
         import torch.distributed as dist
 
@@ -160,7 +266,10 @@ def main():
 
     from authorino_amd import runtime, workloads
 
-    w = workloads.make(args.workload, n=args.n, seed=1000 + rank)
+    # SURVEY.md §8d seeds; rank k > 0 draws its own shard from seed + 7919 k
+    seed = workloads.DEFAULT_SEEDS.get(args.workload, 0) + 7919 * rank
+    unique = args.unique or (4096 if args.workload == "c5" else 16384)
+    w = workloads.make(args.workload, n=args.n, seed=seed, unique=unique, uniquify=True)
     ctx = runtime.Context(local)
     phase = w.auth_config is not None  # c5: the whole authorization phase per request
     if phase:
@@ -221,11 +330,12 @@ def main():
     except (OSError, ValueError):
         pass
 
-    cpu, parity = None, None
+    cpu, parity, c1, pcie = None, None, None, None
     extra = {}
+    tri_h = tri.cpu().numpy()
     if phase:
         # the phase decision from the per-tree results (auth_pipeline.go:454-457, :287-322)
-        t = tri.cpu().numpy().reshape(w.n, nt)[:, :nt_out]  # (the last tree: response selectors)
+        t = tri_h.reshape(w.n, nt)[:, :nt_out]  # (the last tree: response selectors)
         skipped = t[:, 0] != runtime.T
         ok = np.ones(w.n, dtype=bool)
         for k in range(len(cfg.authorization)):
@@ -235,8 +345,21 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu:
             cpu, parity = phase_cpu_baseline(w, exprs, args.cpu_seconds, t)
     elif rank == 0 and world == 1 and not args.no_cpu:
-        cpu, parity = cpu_baseline(w, rpr, args.cpu_seconds, tri.cpu().numpy(), bm.cpu().numpy().view(np.uint64))
-    undecided = int((tri == runtime.UNDECIDED).sum().item())
+        cpu, parity = cpu_baseline(w, rpr, args.cpu_seconds, tri_h, bm.cpu().numpy().view(np.uint64))
+    if rank == 0 and world == 1 and not args.no_cpu:
+        c1 = c1_cpu_ns_per_op()
+    if rank == 0 and world == 1 and not args.no_pcie and not phase:
+        # authjx_eval_batch from host buffers: H2D copy of the arena + kernels + D2H of the
+        # results, synchronous (never the bench value)
+        torch.cuda.synchronize(dev)
+        ctx.eval_host_arena(rss, w.arena, w.offs, w.lens, set_of_req=w.set_of_req)
+        t0 = time.perf_counter()
+        ctx.eval_host_arena(rss, w.arena, w.offs, w.lens, set_of_req=w.set_of_req)
+        dt = time.perf_counter() - t0
+        pcie = {"value": int(rpr.sum()) / dt, "unit": "request×rule evals/s", "ms_per_batch": dt * 1e3,
+                "decisions_per_s": w.n / dt,
+                "note": "authjx_eval_batch from pageable host buffers (H2D arena copy + kernels + D2H), one GPU"}
+    undecided = int((tri_h == runtime.UNDECIDED).sum())
     exact_path = ctx.last_exact_count()  # requests the single-pass kernel handed to the exact scan
 
     if rank == 0:
@@ -258,6 +381,8 @@ def main():
                 "workload": args.workload,
                 "description": w.description,
                 "requests_per_gpu": w.n,
+                "unique_templates": unique,
+                "seed_rank0": workloads.DEFAULT_SEEDS.get(args.workload, 0),
                 "patterns": int(rpr.max()) if w.set_of_req is None else float(rpr.mean()),
                 "selectors": rss[0].n_selectors if len(rss) == 1 else float(np.mean([r.n_selectors for r in rss])),
                 "auth_configs": len(rss),
@@ -277,6 +402,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "parity": parity,
+            "c1_cpu": c1,
+            "pcie_inclusive": pcie,
             "undecided": undecided,
             **extra,
             "exact_path_requests": exact_path,

@@ -130,34 +130,40 @@ int or_pattern_matches(or_ruleset* rs, uint32_t i, const char* json, size_t jlen
 }
 
 /* Recursive Matches with the reference's short-circuit order. Result T/F/E/UNSUPPORTED;
- * *errp = pattern index whose error decided. */
-static int node_matches(or_ruleset* rs, int32_t n, const char* json, size_t jlen, scratch* sc,
-                        int32_t* errp) {
+ * *errp = pattern index whose error decided. res (may be NULL): every pattern's result
+ * already evaluated once (the batch driver's bitmap pass), read instead of re-evaluating. */
+static int node_matches_r(or_ruleset* rs, int32_t n, const char* json, size_t jlen, scratch* sc,
+                          int32_t* errp, const uint8_t* res) {
     const or_node* nd = &rs->nodes[n];
     if (nd->kind == OR_NODE_PATTERN) {
-        int r = pattern_matches(rs, (uint32_t)nd->pattern, json, jlen, sc);
+        int r = res ? res[nd->pattern] : pattern_matches(rs, (uint32_t)nd->pattern, json, jlen, sc);
         if (r == OR_E || r == OR_UNSUPPORTED) *errp = nd->pattern;
         return r;
     }
     if (nd->kind == OR_NODE_AND) {
         if (nd->left >= 0) {
-            int l = node_matches(rs, nd->left, json, jlen, sc, errp);
+            int l = node_matches_r(rs, nd->left, json, jlen, sc, errp, res);
             if (l != OR_T) return l;
         }
         if (nd->right >= 0) {
-            int r = node_matches(rs, nd->right, json, jlen, sc, errp);
+            int r = node_matches_r(rs, nd->right, json, jlen, sc, errp, res);
             if (r != OR_T) return r;
         }
         return OR_T;
     }
     /* Or */
     if (nd->left >= 0) {
-        int l = node_matches(rs, nd->left, json, jlen, sc, errp);
+        int l = node_matches_r(rs, nd->left, json, jlen, sc, errp, res);
         if (l == OR_E || l == OR_UNSUPPORTED) return l;
         if (l == OR_T) return OR_T;
     }
-    if (nd->right >= 0) return node_matches(rs, nd->right, json, jlen, sc, errp);
+    if (nd->right >= 0) return node_matches_r(rs, nd->right, json, jlen, sc, errp, res);
     return OR_F;
+}
+
+static int node_matches(or_ruleset* rs, int32_t n, const char* json, size_t jlen, scratch* sc,
+                        int32_t* errp) {
+    return node_matches_r(rs, n, json, jlen, sc, errp, NULL);
 }
 
 int or_expression_matches(or_ruleset* rs, const char* json, size_t jlen, int32_t* err_pattern) {
@@ -191,19 +197,30 @@ static void* run_job(void* arg) {
     job* j = (job*)arg;
     scratch sc;
     memset(&sc, 0, sizeof sc);
+    uint8_t* res = NULL;
+    uint32_t res_cap = 0;
     for (uint32_t r = j->lo; r < j->hi; r++) {
         or_ruleset* rs = j->sets[j->set_of_req ? j->set_of_req[r] : 0];
         const char* doc = (const char*)j->arena + j->offs[r];
         size_t len = j->lens[r];
+        const uint8_t* cached = NULL;
         if (j->out_bitmap) {
+            /* every pattern once: the bitmap, then the tree walk reads these results */
+            if (rs->n_pats > res_cap) {
+                res_cap = rs->n_pats;
+                res = (uint8_t*)realloc(res, res_cap);
+            }
             uint64_t* row = j->out_bitmap + (size_t)r * j->stride;
             memset(row, 0, j->stride * sizeof(uint64_t));
-            for (uint32_t p = 0; p < rs->n_pats; p++)
-                if (pattern_matches(rs, p, doc, len, &sc) == OR_T) row[p >> 6] |= 1ull << (p & 63);
+            for (uint32_t p = 0; p < rs->n_pats; p++) {
+                res[p] = (uint8_t)pattern_matches(rs, p, doc, len, &sc);
+                if (res[p] == OR_T) row[p >> 6] |= 1ull << (p & 63);
+            }
+            cached = res;
         }
         int32_t ep = -1;
         int t = OR_T;
-        if (rs->root >= 0) t = node_matches(rs, rs->root, doc, len, &sc, &ep);
+        if (rs->root >= 0) t = node_matches_r(rs, rs->root, doc, len, &sc, &ep, cached);
         if (t != OR_E && t != OR_UNSUPPORTED) ep = -1;
         j->out_tristate[r] = (uint8_t)t;
         if (j->out_err_idx) j->out_err_idx[r] = ep;
@@ -211,6 +228,7 @@ static void* run_job(void* arg) {
     or_result_free(&sc.v);
     or_result_free(&sc.item);
     or_buf_free(&sc.s);
+    free(res);
     return NULL;
 }
 

@@ -28,7 +28,7 @@ def _rank_main(rank, world, port, out):
     import bench
     from authorino_amd import workloads
 
-    w = workloads.make("c2", n=64, seed=1000 + rank)  # the shard bench.py gives this rank
+    w = workloads.make("c2", n=64, seed=workloads.DEFAULT_SEEDS["c2"] + 7919 * rank)  # the shard bench.py gives this rank
     delay = 0.02 * (rank + 1)
     calls = []
 
@@ -51,3 +51,26 @@ def test_two_rank_timing_and_shards(tmp_path):
     assert r[0]["elapsed"] == r[1]["elapsed"]  # max over ranks, reported identically
     assert r[0]["elapsed"] >= 4 * 0.04 * 0.95  # at least the slower rank's timed steps
     assert r[0]["first_doc"] != r[1]["first_doc"]  # independent shards
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus2_relaunches_two_ranks():
+    """`bench.py --gpus 2` without a torch.distributed.run environment starts two ranks
+    itself (torch.distributed.run child), each with its own shard; rank 0 prints one JSON
+    line with n_gpus 2. --dry-run keeps the GPU out (gloo, stand-in step)."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--workload", "c2", "--n", "96", "--steps", "3", "--warmup", "1"],
+                         capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 3 and rec["warmup"] == 1 and rec["scaling"] == "weak"
+    shards = rec["shards"]
+    assert [s["rank"] for s in shards] == [0, 1]
+    assert shards[0]["seed"] != shards[1]["seed"]
+    assert shards[0]["first_doc_sha"] != shards[1]["first_doc_sha"]  # independent shards
+    assert all(s["n"] == 96 for s in shards)
