@@ -6,12 +6,15 @@
 //                Requests it can not prove gjson-equivalent go to a slow list.
 // ajx_patterns   stage B, one work-item per request: patterns on the captured values,
 //                T bitmap, And/Or fold.
+// ajx_wave_eval  the wave kernel (ajx_wave.h, the default): wavefront-per-request lexer,
+//                work-item-per-request token walk + patterns + fold
 // ajx_eval_scan  one work-item per request on the slow list (or on every request when
 //                forced): for each selector an exact gjson.Get scan (ajx_device.h gj_get),
 //                then the patterns and the fold. Exact for arbitrary input bytes.
 #include <hip/hip_runtime.h>
 
 #include "ajx_fast.h"
+#include "ajx_wave.h"
 #include "ajx_kernels.h"
 
 namespace ajx {
@@ -312,6 +315,185 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
         }
         finish_request(r, gblob, d, row, out_tri, out_err, out_bm, stride);
     }
+}
+
+// ---------------------------------------------------------------------------------
+// The wave kernel. Each wavefront owns kWaveReqs consecutive requests. It lexes them one
+// after another (all 64 lanes on one document, ajx_wave.h lex_doc) into its LDS token
+// buffer until the buffer or the batch is full, then every lane walks one request's
+// tokens (walk_doc), evaluates its patterns and writes its outputs. Dynamic LDS:
+// [ruleset blob (SHARED)] then per wave [ring 2 KiB | tokens tok_cap x u32 | labels
+// tok_cap x u8 | batch table 64 x 16 B | capture rows 64 x row_stride x u64].
+// ---------------------------------------------------------------------------------
+struct WaveHw {
+    __device__ uint32_t lane() const { return threadIdx.x & 63u; }
+    __device__ uint64_t ballot(bool b) const { return __ballot(b); }
+    __device__ bool any(bool b) const { return __ballot(b) != 0; }
+    __device__ uint32_t shfl_up(uint32_t v) const { return __shfl_up(v, 1); }
+    __device__ uint32_t shfl_down(uint32_t v) const { return __shfl_down(v, 1); }
+    __device__ uint32_t readlane(uint32_t v, uint32_t l) const { return __builtin_amdgcn_readlane(v, l); }
+    __device__ uint32_t bpermute(uint32_t v, uint32_t src) const {
+        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+    }
+    __device__ uint32_t excl_sum(uint32_t v, uint32_t* total) const {
+        uint32_t x = v;
+        const uint32_t l = lane();
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            x += l >= o ? y : 0u;
+        }
+        *total = __builtin_amdgcn_readlane(x, 63);
+        return x - v;
+    }
+    __device__ uint64_t lanemask_lt() const {
+        const uint32_t l = lane();
+        return l ? (~0ull >> (64 - l)) : 0ull;
+    }
+    __device__ uint32_t mbcnt(uint64_t m) const {
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    }
+    __device__ void lds_fence() const {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+};
+
+constexpr uint32_t kWaveBlock = 256;  // 4 wavefronts
+constexpr uint32_t kWaveReqs = 64;    // requests per wavefront (one walker lane each)
+constexpr uint32_t kWaveRing = 2 * kWaveChunk;
+#ifndef AJX_WAVE_LDS
+#define AJX_WAVE_LDS (16 * 1024)  // LDS per wavefront (2 workgroups = 8 waves per CU)
+#endif
+
+struct WaveBatch {
+    uint32_t req, tok_start, tok_cnt, status;
+};
+
+// token-buffer entries of a wave with wave_bytes of LDS and batches of up to nbatch requests
+__host__ __device__ inline uint32_t wave_tok_cap(uint32_t wave_bytes, uint32_t row_stride, uint32_t nbatch) {
+    const uint32_t fixed = kWaveRing + nbatch * ((uint32_t)sizeof(WaveBatch) + row_stride * 8u);
+    return wave_bytes > fixed + 16 ? ((wave_bytes - fixed) / 5u) & ~15u : 0u;
+}
+
+template <bool SHARED>
+__global__ __launch_bounds__(kWaveBlock) void ajx_wave_eval(
+    const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req, const uint8_t* __restrict__ arena,
+    const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n, uint8_t* __restrict__ out_tri,
+    int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm, uint32_t stride, uint64_t* __restrict__ rows_out,
+    uint32_t row_stride, uint32_t* __restrict__ slow_count, uint32_t* __restrict__ slow_ids, uint32_t blob_region,
+    uint32_t wave_bytes, uint32_t nbatch, uint32_t ablate) {
+    extern __shared__ uint4 s_wave[];
+    const uint8_t* blob0 = stage_blob<SHARED>(sets[0]);
+    WaveHw w;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint8_t* base = reinterpret_cast<uint8_t*>(s_wave) + blob_region + (threadIdx.x >> 6) * wave_bytes;
+    const uint32_t tok_cap = wave_tok_cap(wave_bytes, row_stride, nbatch);
+    uint8_t* ring = base;
+    uint32_t* tok = reinterpret_cast<uint32_t*>(base + kWaveRing);
+    uint8_t* lab = base + kWaveRing + tok_cap * 4u;
+    WaveBatch* batch = reinterpret_cast<WaveBatch*>(base + kWaveRing + tok_cap * 5u);
+    uint64_t* rows = reinterpret_cast<uint64_t*>(base + kWaveRing + tok_cap * 5u + nbatch * sizeof(WaveBatch));
+    const uint32_t wid = blockIdx.x * (kWaveBlock / 64u) + (threadIdx.x >> 6);
+    const uint32_t r0 = wid * kWaveReqs;
+    const uint32_t r1 = r0 + kWaveReqs < n ? r0 + kWaveReqs : n;
+    uint32_t i = r0;
+    while (i < r1) {
+        // ---- lex a batch (all lanes on one request at a time) ----
+        uint32_t nb = 0, used = 0;
+        while (i < r1 && nb < nbatch) {
+            const uint32_t r = i;
+            const uint8_t* blob = SHARED ? blob0 : sets[set_of_req ? set_of_req[r] : 0];
+            uint32_t cnt = 0, st;
+            if (!(reinterpret_cast<const RulesetHdr*>(blob)->flags & kFlagWaveOk)) st = LEX_BAD;
+            else st = lex_doc(w, blob, arena + offs[r], lens[r], ring, tok, lab, used, tok_cap, &cnt, ablate & 3u);
+            if (st == LEX_OVERFLOW && nb > 0) break;  // this request starts the next batch
+            if (lane == 0) batch[nb] = WaveBatch{r, used, cnt, st};
+            if (st == LEX_OK) used += cnt;
+            nb++;
+            i++;
+        }
+        w.lds_fence();
+        if (ablate) {  // profiling: lexer only
+            if (lane < nb) out_tri[batch[lane].req] = (uint8_t)batch[lane].status;
+            w.lds_fence();
+            continue;
+        }
+        // ---- walk + patterns: one request per lane ----
+        if (lane < nb) {
+            const WaveBatch b = batch[lane];
+            const uint32_t r = b.req;
+            const uint8_t* blob = SHARED ? blob0 : sets[set_of_req ? set_of_req[r] : 0];
+            const uint8_t* d = arena + offs[r];
+            uint64_t* row = rows + (size_t)lane * row_stride;
+            const bool ok = b.status == LEX_OK &&
+                            walk_doc(blob, blob_tables(blob), tok, lab, b.tok_start, b.tok_start + b.tok_cnt, d, row);
+            if (!ok) {
+                row[0] = kRowSlow;
+                slow_ids[atomicAdd(slow_count, 1u)] = r;
+            } else {
+                finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride);
+            }
+            if (rows_out) {
+                uint64_t* g = rows_out + (size_t)r * row_stride;
+                const uint32_t ns = reinterpret_cast<const RulesetHdr*>(blob)->n_selectors;
+                g[0] = row[0];
+                for (uint32_t s = 0; s < ns && ok; s++) g[1 + s] = row[1 + s];
+            }
+        }
+        w.lds_fence();
+    }
+}
+
+hipError_t launch_eval_wave(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
+                            const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                            uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows_out,
+                            uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
+                            uint32_t wave_lds_bytes, uint32_t ablate) {
+    if (n == 0) return hipSuccess;
+    const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
+    // batch size and LDS per wave: the capture rows of a batch take at most a third of it,
+    // the token buffer holds at least 1024 tokens (~8 KiB of compact JSON)
+    uint32_t wave_bytes = wave_lds_bytes ? wave_lds_bytes : AJX_WAVE_LDS, nbatch = 0;
+    for (;; wave_bytes += 4096) {
+        nbatch = (wave_bytes / 3) / (row_stride * 8u + (uint32_t)sizeof(WaveBatch));
+        nbatch = nbatch > kWaveReqs ? kWaveReqs : nbatch < 8 ? 8u : nbatch;
+        if (wave_tok_cap(wave_bytes, row_stride, nbatch) >= 1024 || wave_bytes > 36 * 1024) break;
+    }
+    if (wave_tok_cap(wave_bytes, row_stride, nbatch) < 256) return hipErrorInvalidValue;
+    const uint32_t blob_region = shared ? (shared_blob_bytes + 15u) & ~15u : 0u;
+    const uint32_t lds = blob_region + (kWaveBlock / 64) * wave_bytes;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    // (per device: the attribute belongs to the device's code object)
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    static bool attr_set[64] = {};
+    if (dev >= 0 && dev < 64 && !attr_set[dev]) {
+        const void* ks[] = {reinterpret_cast<const void*>(&ajx_wave_eval<true>),
+                            reinterpret_cast<const void*>(&ajx_wave_eval<false>)};
+        for (const void* k : ks)
+            if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
+                return e;
+        attr_set[dev] = true;
+    }
+    const uint32_t waves = (n + kWaveReqs - 1) / kWaveReqs;
+    const uint32_t grid = (waves + kWaveBlock / 64 - 1) / (kWaveBlock / 64);
+    if (shared)
+        hipLaunchKernelGGL((ajx_wave_eval<true>), dim3(grid), dim3(kWaveBlock), lds, stream, d_sets, d_set_of_req,
+                           d_arena, d_offs, d_lens, n, d_tri, d_err, d_bm, stride, d_rows_out, row_stride,
+                           d_slow_count, d_slow_ids, blob_region, wave_bytes, nbatch, ablate);
+    else
+        hipLaunchKernelGGL((ajx_wave_eval<false>), dim3(grid), dim3(kWaveBlock), lds, stream, d_sets, d_set_of_req,
+                           d_arena, d_offs, d_lens, n, d_tri, d_err, d_bm, stride, d_rows_out, row_stride,
+                           d_slow_count, d_slow_ids, blob_region, wave_bytes, nbatch, ablate);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
+    hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(256), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
+                       d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------

@@ -46,6 +46,8 @@ def parse():
                     help="distinct document templates (default 16384 for c2/c3/c4, 4096 for c5)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo test of the distributed driver: no GPU, a stand-in step")
+    ap.add_argument("--kernel-mode", type=int, default=0,
+                    help="profiling: 0 the wave kernel (default), 6 the round-1 single-pass kernel")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -271,6 +273,8 @@ def main():
     unique = args.unique or (4096 if args.workload == "c5" else 16384)
     w = workloads.make(args.workload, n=args.n, seed=seed, unique=unique, uniquify=True)
     ctx = runtime.Context(local)
+    if args.kernel_mode:
+        ctx.set_kernel_mode(args.kernel_mode)
     phase = w.auth_config is not None  # c5: the whole authorization phase per request
     if phase:
         # one forest ruleset: top-level when, each evaluator's when and rules, and last the
