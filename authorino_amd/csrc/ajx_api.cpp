@@ -48,9 +48,8 @@ struct authjx_ctx {
     const authjx_ruleset* rows_rs = nullptr;
     uint32_t rows_n = 0, rows_stride = 0;
     int force_scan = 0;
-    int ablate = 0;  // profiling only: 1/2/3 reduced single-pass variants, 6 the single-pass kernel,
-                     // 11/12/14 wave-kernel ablations (ajx_kernels.h launch_eval_wave)
-    uint32_t wave_lds = 0;  // profiling only: LDS per wave of the wave kernel (0 = default)
+    int ablate = 0;  // profiling only: 1/2/3 reduced single-pass variants, 20 the lane kernel,
+                     // 21..24 its ablations (ajx_kernels.hip ajx_lane_eval)
     float last_ms = 0.f;
 };
 
@@ -258,48 +257,51 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         if (rc != AUTHJX_OK) return rc;
     }
     HIP_OK(hipEventRecord(ctx->ev0, s));
-    // the wave kernel (default) when every ruleset of the batch has its tables
-    bool wave = !ctx->force_scan && (ctx->ablate == 0 || ctx->ablate >= 10);
-    for (uint32_t i = 0; i < n_sets && wave; i++)
-        wave = (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagWaveOk) != 0;
-    // capture rows kept for authjx_select_from_eval_device: single-pass kernel, one
-    // ruleset; the wave kernel writes them out for forests (an authorization phase whose
-    // last tree holds the response selectors) only
-    const bool keep_rows = !ctx->force_scan && n_sets == 1 && (ctx->ablate == 0 || ctx->ablate == 6) &&
-                           (!wave || sets[0]->c.n_trees > 1);
+    // kernel: the single-pass kernel (default; ajx_scan_fused); ablate 20 the lane
+    // kernel (21..24 its ablations), 1..3 single-pass ablations
+    bool fast_tables = !ctx->force_scan;
+    for (uint32_t i = 0; i < n_sets && fast_tables; i++)
+        fast_tables = (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagFastOk) != 0;
+    const bool lane = fast_tables && ctx->ablate >= 20;
+    // capture rows kept for authjx_select_from_eval_device: one ruleset, a full kernel
+    const bool full = ctx->ablate == 0 || ctx->ablate == 20;
+    const bool keep_rows = !ctx->force_scan && n_sets == 1 && full;
     ctx->rows_rs = keep_rows ? sets[0] : nullptr;
     ctx->rows_n = n;
     ctx->rows_stride = row_stride;
-    if (wave) {
-        size_t max_blob = 0;
-        for (uint32_t i = 0; i < n_sets; i++) max_blob = std::max(max_blob, sets[i]->c.blob.size());
-        const uint32_t stage_bytes = n_sets == 1 && max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u;
-        HIP_OK(ajx::launch_eval_wave(ctx->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
-                                     d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
-                                     keep_rows ? ctx->d_rows : nullptr, row_stride, ctx->d_slow, ctx->d_slow + 1, s,
-                                     ctx->wave_lds, ctx->ablate >= 10 ? (uint32_t)(ctx->ablate - 10) : 0u));
-    } else if (ctx->force_scan)
+    size_t max_blob = 0;
+    for (uint32_t i = 0; i < n_sets; i++) max_blob = std::max(max_blob, sets[i]->c.blob.size());
+    if (ctx->force_scan) {
         HIP_OK(ajx::launch_eval_scan(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
-    else {
+    } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
-        // caller's bucketing by AuthConfig), the default kernel, batches worth sorting
+        // caller's bucketing by AuthConfig), a full kernel, batches worth sorting
         const uint32_t* perm = nullptr;
-        if (ctx->len_sort && (n_sets == 1 || ctx->len_sort > 1) && (ctx->ablate == 0 || ctx->ablate == 6) && n >= 4096) {
+        if (ctx->len_sort && (n_sets == 1 || ctx->len_sort > 1) && full && n >= 4096) {
             HIP_OK(ajx::launch_len_order(d_lens, n, ctx->d_perm + n, ctx->d_perm, s));
             perm = ctx->d_perm;
         }
-        // uniform batch: the blob staged once per workgroup; multi-tenant batch: the largest
-        // blob, for workgroups whose requests share one ruleset (ajx_scan_fused_tenant)
-        size_t max_blob = 0;
-        for (uint32_t i = 0; i < n_sets; i++) max_blob = std::max(max_blob, sets[i]->c.blob.size());
-        const uint32_t stage_bytes =
-            n_sets == 1 ? (max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u)
-                        : (!ctx->no_tenant_stage && max_blob <= ajx::kMaxTenantStageBytes ? (uint32_t)max_blob : 0u);
-        HIP_OK(ajx::launch_eval_fast(
-            ctx->d_sets, d_set_of_req, stage_bytes,
-            d_arena, d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words, ctx->d_rows,
-            row_stride, ctx->d_slow, ctx->d_slow + 1, s, ctx->ablate == 6 ? 0 : ctx->ablate, perm));
+        if (lane) {
+            const uint32_t stage_bytes =
+                n_sets == 1 && max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u;
+            HIP_OK(ajx::launch_eval_lane(ctx->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
+                                         d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
+                                         ctx->d_rows, row_stride, ctx->d_slow, ctx->d_slow + 1, s,
+                                         ctx->ablate - 20, perm));
+        } else {
+            // uniform batch: the blob staged once per workgroup; multi-tenant batch: the
+            // largest blob, for workgroups whose requests share one ruleset
+            // (ajx_scan_fused_tenant)
+            const uint32_t stage_bytes =
+                n_sets == 1 ? (max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u)
+                            : (!ctx->no_tenant_stage && max_blob <= ajx::kMaxTenantStageBytes ? (uint32_t)max_blob
+                                                                                              : 0u);
+            HIP_OK(ajx::launch_eval_fast(ctx->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
+                                         d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
+                                         ctx->d_rows, row_stride, ctx->d_slow, ctx->d_slow + 1, s,
+                                         ctx->ablate < 20 ? ctx->ablate : 0, perm));
+        }
     }
     HIP_OK(hipEventRecord(ctx->ev1, s));
     return AUTHJX_OK;
@@ -414,14 +416,6 @@ int authjx_debug_ablate(authjx_ctx* ctx, int mode) {
     return AUTHJX_OK;
 }
 
-// Profiling only (not in authjx.h): LDS bytes per wavefront of the wave kernel (token
-// buffer size; 0 = the default).
-int authjx_debug_wave_lds(authjx_ctx* ctx, uint32_t bytes) {
-    if (!ctx) return AUTHJX_EINVAL;
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    ctx->wave_lds = bytes;
-    return AUTHJX_OK;
-}
 
 // Profiling only (not in authjx.h): the length-bucketed request order off (0), for
 // single-ruleset batches (1, default) or for every batch (2).

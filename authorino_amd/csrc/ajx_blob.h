@@ -144,24 +144,6 @@ struct SelectorPatterns {
     uint64_t mask[2];      // the same patterns as a bitmask
 };
 
-// ---- wave kernel (ajx_wave.h): key labels and trie edges ----------------------
-// Every distinct object key of the trie (its unescaped bytes) has a label id 1..n_labels
-// (0 = a key no selector component names). The lexer looks a key up once by (length,
-// last <= 8 bytes) in the label table; the walker moves from node to child through the
-// edge table keyed by (node, label).
-struct LabelSlot {
-    uint64_t sig;      // key_signature(key)
-    uint32_t meta;     // key_len | label << 16; kEmptySlot = free
-    uint32_t key_off;  // key bytes in the literal pool
-};
-static_assert(sizeof(LabelSlot) == 16, "LabelSlot layout");
-constexpr uint32_t kEmptyEdge = 0xFFFFFFFFu;  // edge slot: node | label << 8 | child << 16
-constexpr uint32_t kMaxLabels = 254;
-
-AJX_BLOB_HD inline uint32_t edge_hash(uint32_t node, uint32_t label, uint32_t log2) {
-    return ((node * 0x9E3779B1u) ^ (label * 0x85EBCA77u)) >> (32 - log2);
-}
-
 struct RulesetHdr {
     uint32_t magic;
     uint32_t total_bytes;
@@ -176,7 +158,7 @@ struct RulesetHdr {
     uint32_t off_literals;
     uint32_t lit_bytes;
     uint32_t n_components;
-    uint32_t flags;  // bit0: has regex; bit1: has unsupported pattern; bit2: fast path ok; bit3: wave kernel ok
+    uint32_t flags;  // bit0: has regex; bit1: has unsupported pattern; bit2: fast path ok
     uint32_t n_trie_nodes;
     uint32_t off_trie_nodes;
     uint32_t off_trie_children;
@@ -185,17 +167,11 @@ struct RulesetHdr {
     uint32_t key_slots_log2;    // KeySlot table of 1 << key_slots_log2 entries
     uint32_t off_key_slots;
     uint32_t pad1[3];
-    uint32_t n_labels;          // wave kernel: label table (LabelSlot, 1 << label_slots_log2)
-    uint32_t label_slots_log2;
-    uint32_t off_label_slots;
-    uint32_t edge_slots_log2;   // edge table (u32, 1 << edge_slots_log2)
-    uint32_t off_edge_slots;
-    uint32_t pad2[3];
+    uint32_t pad2[8];
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
     uint64_t unsupported[2];    // pattern p can not be decided on the device
 };
 constexpr uint32_t kFlagFastOk = 4;
-constexpr uint32_t kFlagWaveOk = 8;  // eligible for the wave kernel (labels and edges built)
 
 }  // namespace ajx

@@ -385,7 +385,8 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 const std::string& key = trie[i].keys[j].first;
                 ch.sig = key_signature((const uint8_t*)key.data(), (uint32_t)key.size());
                 ch.key_len = (uint32_t)key.size();
-                while (lits.size() % 4) lits.push_back('\0');
+                // (8-byte aligned: the lane kernel compares long keys a word at a time)
+                while (lits.size() % 8) lits.push_back('\0');
                 ch.key_off = (uint32_t)lits.size();
                 lits += key;
                 ch.array_index = trie[i].keys[j].second;
@@ -410,57 +411,6 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             }
         }
         hdr.key_slots_log2 = log2;
-        // wave kernel: one label per distinct key, the edges (node, label) -> child
-        std::map<std::string, uint32_t> label_of;
-        std::vector<uint32_t> label_off;
-        for (size_t i = 0; i < trie.size(); i++)
-            for (uint32_t j = 0; j < tn[i].n_children; j++) {
-                const TrieChild& ch = tc[tn[i].child_begin + j];
-                const std::string key = trie[i].keys[j].first;
-                if (!label_of.count(key)) {
-                    const uint32_t id = (uint32_t)label_of.size() + 1;
-                    label_of[key] = id;
-                    label_off.push_back(ch.key_off);
-                }
-            }
-        const bool wave_ok = fast_ok && label_of.size() <= kMaxLabels;
-        uint32_t llog2 = 4;
-        while ((1u << llog2) < 2 * label_of.size()) llog2++;
-        std::vector<LabelSlot> lslots(1u << llog2);
-        for (LabelSlot& l : lslots) { l.sig = 0; l.meta = kEmptySlot; l.key_off = 0; }
-        uint32_t n_edges = 0;
-        for (size_t i = 0; i < trie.size(); i++) n_edges += tn[i].n_children;
-        uint32_t elog2 = 4;
-        while ((1u << elog2) < 2 * n_edges) elog2++;
-        std::vector<uint32_t> eslots(1u << elog2, kEmptyEdge);
-        if (wave_ok) {
-            size_t li = 0;
-            for (const auto& kv : label_of) {
-                (void)li;
-                const std::string& key = kv.first;
-                const uint64_t sig = key_signature((const uint8_t*)key.data(), (uint32_t)key.size());
-                uint32_t at = key_slot_hash(sig, (uint32_t)key.size(), 0, llog2);
-                while (lslots[at].meta != kEmptySlot) at = (at + 1) & ((1u << llog2) - 1);
-                lslots[at].sig = sig;
-                lslots[at].meta = (uint32_t)key.size() | (kv.second << 16);
-                lslots[at].key_off = label_off[kv.second - 1];
-            }
-            for (size_t i = 0; i < trie.size(); i++)
-                for (uint32_t j = 0; j < tn[i].n_children; j++) {
-                    const uint32_t lab = label_of[trie[i].keys[j].first];
-                    uint32_t at = edge_hash((uint32_t)i, lab, elog2);
-                    while (eslots[at] != kEmptyEdge) at = (at + 1) & ((1u << elog2) - 1);
-                    eslots[at] = (uint32_t)i | (lab << 8) | (trie[i].kids[j] << 16);
-                }
-            flags |= kFlagWaveOk;
-        }
-        hdr.n_labels = (uint32_t)label_of.size();
-        hdr.label_slots_log2 = llog2;
-        hdr.off_label_slots = (uint32_t)b.align16();
-        b.append(lslots.data(), lslots.size() * sizeof(LabelSlot));
-        hdr.edge_slots_log2 = elog2;
-        hdr.off_edge_slots = (uint32_t)b.align16();
-        b.append(eslots.data(), eslots.size() * sizeof(uint32_t));
         hdr.n_trie_nodes = (uint32_t)tn.size();
         hdr.off_trie_nodes = (uint32_t)b.align16();
         b.append(tn.data(), tn.size() * sizeof(TrieNode));

@@ -46,18 +46,18 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
                             int mode = 0, const uint32_t* d_perm = nullptr);
 
-// The wave kernel (ajx_wave.h): one wavefront per request for the structural scan, one
-// work-item per request for the token walk and the patterns; requests it can not prove
-// valid compact JSON go to the exact scan (launched after it on the stream).
-// shared_blob_bytes as for launch_eval_fast. d_rows_out (may be null): the capture rows,
-// row_stride u64 per request, for authjx_select_from_eval_device. wave_lds_bytes: LDS per
-// wave (ring + token buffer + batch rows), 0 = default. ablate (profiling, outputs
-// meaningless): 4 the lexer alone, 1 the lexer without tokens, 2 the loads alone.
-hipError_t launch_eval_wave(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
+// The lane kernel (ajx_lane.h): one work-item per request over 64-byte windows the
+// wavefront stages through LDS with coalesced loads; stage B in the same work-item;
+// requests it can not prove valid compact JSON go to the exact scan (launched after it).
+// d_rows: capture rows (row_stride u64 per request, kept for authjx_select_from_eval).
+// d_perm (may be null): length-bucketed request order. mode (profiling, uniform ruleset
+// only, outputs meaningless): 1 the window staging alone, 2 no token walk and no stage B,
+// 3 no key lookups, 4 no stage B.
+hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
-                            uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows_out,
+                            uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            uint32_t wave_lds_bytes = 0, uint32_t ablate = 0);
+                            int mode = 0, const uint32_t* d_perm = nullptr);
 
 // Length-bucketed request order for the single-pass kernel: d_perm[n] = request ids,
 // longest 8-byte length class first; d_hist needs 2 * 1024 + 1 u32 of scratch.

@@ -6,15 +6,15 @@
 //                Requests it can not prove gjson-equivalent go to a slow list.
 // ajx_patterns   stage B, one work-item per request: patterns on the captured values,
 //                T bitmap, And/Or fold.
-// ajx_wave_eval  the wave kernel (ajx_wave.h, the default): wavefront-per-request lexer,
-//                work-item-per-request token walk + patterns + fold
+// ajx_lane_eval  the lane kernel (ajx_lane.h): work-item per request over 64-byte
+//                windows the wavefront stages through LDS with coalesced loads
 // ajx_eval_scan  one work-item per request on the slow list (or on every request when
 //                forced): for each selector an exact gjson.Get scan (ajx_device.h gj_get),
 //                then the patterns and the fold. Exact for arbitrary input bytes.
 #include <hip/hip_runtime.h>
 
 #include "ajx_fast.h"
-#include "ajx_wave.h"
+#include "ajx_lane.h"
 #include "ajx_kernels.h"
 
 namespace ajx {
@@ -317,42 +317,12 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     }
 }
 
-// ---------------------------------------------------------------------------------
-// The wave kernel. Each wavefront owns kWaveReqs consecutive requests. It lexes them one
-// after another (all 64 lanes on one document, ajx_wave.h lex_doc) into its LDS token
-// buffer until the buffer or the batch is full, then every lane walks one request's
-// tokens (walk_doc), evaluates its patterns and writes its outputs. Dynamic LDS:
-// [ruleset blob (SHARED)] then per wave [ring 2 KiB | tokens tok_cap x u32 | labels
-// tok_cap x u8 | batch table 64 x 16 B | capture rows 64 x row_stride x u64].
-// ---------------------------------------------------------------------------------
+// wavefront helpers of the lane kernel's window staging
 struct WaveHw {
-    __device__ uint32_t lane() const { return threadIdx.x & 63u; }
-    __device__ uint64_t ballot(bool b) const { return __ballot(b); }
-    __device__ bool any(bool b) const { return __ballot(b) != 0; }
-    __device__ uint32_t shfl_up(uint32_t v) const { return __shfl_up(v, 1); }
-    __device__ uint32_t shfl_down(uint32_t v) const { return __shfl_down(v, 1); }
-    __device__ uint32_t readlane(uint32_t v, uint32_t l) const { return __builtin_amdgcn_readlane(v, l); }
     __device__ uint32_t bpermute(uint32_t v, uint32_t src) const {
         return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
     }
-    __device__ uint32_t excl_sum(uint32_t v, uint32_t* total) const {
-        uint32_t x = v;
-        const uint32_t l = lane();
-#pragma unroll
-        for (uint32_t o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o);
-            x += l >= o ? y : 0u;
-        }
-        *total = __builtin_amdgcn_readlane(x, 63);
-        return x - v;
-    }
-    __device__ uint64_t lanemask_lt() const {
-        const uint32_t l = lane();
-        return l ? (~0ull >> (64 - l)) : 0ull;
-    }
-    __device__ uint32_t mbcnt(uint64_t m) const {
-        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    }
+    // the wavefront's LDS writes are visible to all its lanes
     __device__ void lds_fence() const {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -360,136 +330,195 @@ struct WaveHw {
     }
 };
 
-constexpr uint32_t kWaveBlock = 256;  // 4 wavefronts
-constexpr uint32_t kWaveReqs = 64;    // requests per wavefront (one walker lane each)
-constexpr uint32_t kWaveRing = 2 * kWaveChunk;
-#ifndef AJX_WAVE_LDS
-#define AJX_WAVE_LDS (16 * 1024)  // LDS per wavefront (2 workgroups = 8 waves per CU)
+// ---------------------------------------------------------------------------------
+// The lane kernel (ajx_lane.h): one work-item per request, 64-byte windows staged by the
+// wavefront. Window w of the wave's 64 requests is four 1 KiB loads: in load q, lane l
+// brings the 16-byte block (l & 3) of window w of request 16 q + (l >> 2) — four lanes
+// read one request's 64 contiguous bytes, so one load instruction touches 16 documents —
+// and writes it to LDS at slot + q KiB + 16 l, which is where request 16 q + j finds its
+// window (q KiB + 64 j). Three slots per wave: window w - 1 (key bytes that started
+// there), window w (being scanned), window w + 1 (the byte after w; staged one window
+// ahead, at the start of iteration w, into the slot of w - 2). Latency: a wave waits for
+// its own window loads while the other waves of its SIMD scan (no registers held across
+// the scan). Dynamic LDS: [ruleset blob (SHARED)] [per wave 3 x 4 KiB].
+// MODE (profiling ablations, outputs meaningless): 1 the staging alone, 2 no token walk
+// and no stage B, 3 no key lookups, 4 no stage B.
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kLaneBlock = 256;
+#ifndef AJX_LANE_WAVES
+#define AJX_LANE_WAVES 4  // waves per SIMD the lane kernel's register budget is set for
 #endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kLaneStageBytes = 3 * kLaneSlot;
 
-struct WaveBatch {
-    uint32_t req, tok_start, tok_cnt, status;
-};
-
-// token-buffer entries of a wave with wave_bytes of LDS and batches of up to nbatch requests
-__host__ __device__ inline uint32_t wave_tok_cap(uint32_t wave_bytes, uint32_t row_stride, uint32_t nbatch) {
-    const uint32_t fixed = kWaveRing + nbatch * ((uint32_t)sizeof(WaveBatch) + row_stride * 8u);
-    return wave_bytes > fixed + 16 ? ((wave_bytes - fixed) / 5u) & ~15u : 0u;
-}
-
-template <bool SHARED>
-__global__ __launch_bounds__(kWaveBlock) void ajx_wave_eval(
-    const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req, const uint8_t* __restrict__ arena,
-    const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n, uint8_t* __restrict__ out_tri,
-    int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm, uint32_t stride, uint64_t* __restrict__ rows_out,
-    uint32_t row_stride, uint32_t* __restrict__ slow_count, uint32_t* __restrict__ slow_ids, uint32_t blob_region,
-    uint32_t wave_bytes, uint32_t nbatch, uint32_t ablate) {
-    extern __shared__ uint4 s_wave[];
-    const uint8_t* blob0 = stage_blob<SHARED>(sets[0]);
-    WaveHw w;
-    const uint32_t lane = threadIdx.x & 63u;
-    uint8_t* base = reinterpret_cast<uint8_t*>(s_wave) + blob_region + (threadIdx.x >> 6) * wave_bytes;
-    const uint32_t tok_cap = wave_tok_cap(wave_bytes, row_stride, nbatch);
-    uint8_t* ring = base;
-    uint32_t* tok = reinterpret_cast<uint32_t*>(base + kWaveRing);
-    uint8_t* lab = base + kWaveRing + tok_cap * 4u;
-    WaveBatch* batch = reinterpret_cast<WaveBatch*>(base + kWaveRing + tok_cap * 5u);
-    uint64_t* rows = reinterpret_cast<uint64_t*>(base + kWaveRing + tok_cap * 5u + nbatch * sizeof(WaveBatch));
-    const uint32_t wid = blockIdx.x * (kWaveBlock / 64u) + (threadIdx.x >> 6);
-    const uint32_t r0 = wid * kWaveReqs;
-    const uint32_t r1 = r0 + kWaveReqs < n ? r0 + kWaveReqs : n;
-    uint32_t i = r0;
-    while (i < r1) {
-        // ---- lex a batch (all lanes on one request at a time) ----
-        uint32_t nb = 0, used = 0;
-        while (i < r1 && nb < nbatch) {
-            const uint32_t r = i;
-            const uint8_t* blob = SHARED ? blob0 : sets[set_of_req ? set_of_req[r] : 0];
-            uint32_t cnt = 0, st;
-            if (!(reinterpret_cast<const RulesetHdr*>(blob)->flags & kFlagWaveOk)) st = LEX_BAD;
-            else st = lex_doc(w, blob, arena + offs[r], lens[r], ring, tok, lab, used, tok_cap, &cnt, ablate & 3u);
-            if (st == LEX_OVERFLOW && nb > 0) break;  // this request starts the next batch
-            if (lane == 0) batch[nb] = WaveBatch{r, used, cnt, st};
-            if (st == LEX_OK) used += cnt;
-            nb++;
-            i++;
-        }
-        w.lds_fence();
-        if (ablate) {  // profiling: lexer only
-            if (lane < nb) out_tri[batch[lane].req] = (uint8_t)batch[lane].status;
-            w.lds_fence();
-            continue;
-        }
-        // ---- walk + patterns: one request per lane ----
-        if (lane < nb) {
-            const WaveBatch b = batch[lane];
-            const uint32_t r = b.req;
-            const uint8_t* blob = SHARED ? blob0 : sets[set_of_req ? set_of_req[r] : 0];
-            const uint8_t* d = arena + offs[r];
-            uint64_t* row = rows + (size_t)lane * row_stride;
-            const bool ok = b.status == LEX_OK &&
-                            walk_doc(blob, blob_tables(blob), tok, lab, b.tok_start, b.tok_start + b.tok_cnt, d, row);
-            if (!ok) {
-                row[0] = kRowSlow;
-                slow_ids[atomicAdd(slow_count, 1u)] = r;
-            } else {
-                finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride);
-            }
-            if (rows_out) {
-                uint64_t* g = rows_out + (size_t)r * row_stride;
-                const uint32_t ns = reinterpret_cast<const RulesetHdr*>(blob)->n_selectors;
-                g[0] = row[0];
-                for (uint32_t s = 0; s < ns && ok; s++) g[1 + s] = row[1 + s];
-            }
-        }
-        w.lds_fence();
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)v, o);
+        v = y > v ? y : v;
     }
+    return v;
 }
 
-hipError_t launch_eval_wave(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
+template <int MODE, bool SHARED>
+__global__ __launch_bounds__(kLaneBlock, AJX_LANE_WAVES) void ajx_lane_eval(
+    const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req, const uint8_t* __restrict__ arena,
+    const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n, uint64_t* __restrict__ rows,
+    uint32_t row_stride, uint32_t* __restrict__ slow_count, uint32_t* __restrict__ slow_ids,
+    uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm, uint32_t stride,
+    uint32_t blob_region, const uint32_t* __restrict__ perm) {
+    extern __shared__ uint4 s_lane[];
+    const uint8_t* blob0 = stage_blob<SHARED>(sets[0]);
+    WaveHw hw;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint8_t* stage = reinterpret_cast<uint8_t*>(s_lane) + blob_region + (threadIdx.x >> 6) * kLaneStageBytes;
+    const uint32_t k = blockIdx.x * kLaneBlock + threadIdx.x;
+    const bool live = k < n;
+    const uint32_t r = live ? (perm ? perm[k] : k) : 0u;
+    const uint8_t* blob = SHARED ? blob0 : sets[set_of_req && live ? set_of_req[r] : 0];
+    const uint8_t* d = arena + (live ? offs[r] : 0);
+    const uint32_t len = live ? lens[r] : 0u;
+    const uint32_t mis = (uint32_t)((uintptr_t)d & 15u);
+    bool act = live && (reinterpret_cast<const RulesetHdr*>(blob)->flags & kFlagFastOk) && len < (1u << 24) && len;
+    const uint32_t nblk = act ? (mis + len + 15u) / 16u : 0u;
+    const uint32_t nwin = act ? (mis + len + kLaneWin - 1u) / kLaneWin : 0u;
+    const uint32_t nwmax = wave_max(nwin);
+    // the requests this lane loads for: 16 q + (lane >> 2), q = 0..3
+    const uintptr_t base = (uintptr_t)(d - mis);
+    const uint4* pb[4];
+    uint32_t pn[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t src = 16u * (uint32_t)q + (lane >> 2);
+        const uint32_t lo = hw.bpermute((uint32_t)base, src), hi = hw.bpermute((uint32_t)((uint64_t)base >> 32), src);
+        pb[q] = reinterpret_cast<const uint4*>((uintptr_t)(((uint64_t)hi << 32) | lo));
+        pn[q] = hw.bpermute(nblk, src);
+    }
+    const uint32_t sub = lane & 3u;
+    auto load_win = [&](uint32_t w, uint4 (&v)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t b = w * 4u + sub;
+            if (b < pn[q]) {
+                const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pb[q]) + b);
+                v[q] = make_uint4(t.x, t.y, t.z, t.w);
+            } else {
+                v[q] = make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
+    };
+    auto store_win = [&](uint32_t w, const uint4 (&v)[4]) {
+        uint4* s = reinterpret_cast<uint4*>(stage + (w % 3u) * kLaneSlot);
+#pragma unroll
+        for (int q = 0; q < 4; q++) s[q * 64 + lane] = v[q];
+    };
+    const uint32_t lane_off = (lane >> 4) * 1024u + (lane & 15u) * kLaneWin;
+    uint64_t* row = rows + (size_t)r * row_stride;
+    LaneScan sc;
+    if (act) sc.init(blob, blob_tables(blob), d, len, row);
+    sc.stage = (const AJX_LDS uint8_t*)stage;
+    sc.lane_off = lane_off;
+    uint32_t acc = 0;  // (MODE 1)
+    for (uint32_t w = 0; w < nwmax; w++) {
+        // stage window w (first iteration) and w + 1: the loads are waited for here;
+        // the other waves of the SIMD scan meanwhile
+        {
+            uint4 pf[4];
+            if (w == 0) {
+                load_win(0, pf);
+                store_win(0, pf);
+            }
+            if (w + 1 < nwmax) {
+                load_win(w + 1, pf);
+                store_win(w + 1, pf);
+            }
+            hw.lds_fence();
+        }
+        if (act && w < nwin) {
+            const uint4* s = reinterpret_cast<const uint4*>(stage + (w % 3u) * kLaneSlot + lane_off);
+            uint32_t x[16];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint4 v = s[j];
+                x[4 * j] = v.x;
+                x[4 * j + 1] = v.y;
+                x[4 * j + 2] = v.z;
+                x[4 * j + 3] = v.w;
+            }
+            if constexpr (MODE == 1) {
+#pragma unroll
+                for (int j = 0; j < 16; j++) acc ^= x[j];
+            } else {
+                sc.template window<MODE == 2 ? 2 : MODE == 3 ? 3 : 0>(x, w);
+                act = !sc.bad;
+            }
+        }
+        hw.lds_fence();  // every lane is done with window w - 1's slot before w + 2 lands there
+    }
+    if (!live) return;
+    if constexpr (MODE == 1) {
+        out_tri[r] = (uint8_t)acc;
+        return;
+    }
+    if (!act || !sc.finish()) {
+        row[0] = kRowSlow;
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
+        return;
+    }
+    if constexpr (MODE == 2 || MODE == 4) {  // profiling: no stage B
+        out_tri[r] = (uint8_t)row[0];
+        return;
+    }
+    finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride);
+}
+
+hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
-                            uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows_out,
+                            uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            uint32_t wave_lds_bytes, uint32_t ablate) {
+                            int mode, const uint32_t* d_perm) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
-    // batch size and LDS per wave: the capture rows of a batch take at most a third of it,
-    // the token buffer holds at least 1024 tokens (~8 KiB of compact JSON)
-    uint32_t wave_bytes = wave_lds_bytes ? wave_lds_bytes : AJX_WAVE_LDS, nbatch = 0;
-    for (;; wave_bytes += 4096) {
-        nbatch = (wave_bytes / 3) / (row_stride * 8u + (uint32_t)sizeof(WaveBatch));
-        nbatch = nbatch > kWaveReqs ? kWaveReqs : nbatch < 8 ? 8u : nbatch;
-        if (wave_tok_cap(wave_bytes, row_stride, nbatch) >= 1024 || wave_bytes > 36 * 1024) break;
-    }
-    if (wave_tok_cap(wave_bytes, row_stride, nbatch) < 256) return hipErrorInvalidValue;
     const uint32_t blob_region = shared ? (shared_blob_bytes + 15u) & ~15u : 0u;
-    const uint32_t lds = blob_region + (kWaveBlock / 64) * wave_bytes;
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const uint32_t lds = blob_region + (kLaneBlock / 64) * kLaneStageBytes;
+    if (lds > 160 * 1024 || (mode != 0 && !shared)) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    // (per device: the attribute belongs to the device's code object)
     int dev = 0;
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     static bool attr_set[64] = {};
     if (dev >= 0 && dev < 64 && !attr_set[dev]) {
-        const void* ks[] = {reinterpret_cast<const void*>(&ajx_wave_eval<true>),
-                            reinterpret_cast<const void*>(&ajx_wave_eval<false>)};
+        const void* ks[] = {reinterpret_cast<const void*>(&ajx_lane_eval<0, true>),
+                            reinterpret_cast<const void*>(&ajx_lane_eval<0, false>),
+                            reinterpret_cast<const void*>(&ajx_lane_eval<1, true>),
+                            reinterpret_cast<const void*>(&ajx_lane_eval<2, true>),
+                            reinterpret_cast<const void*>(&ajx_lane_eval<3, true>),
+                            reinterpret_cast<const void*>(&ajx_lane_eval<4, true>)};
         for (const void* k : ks)
             if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
                 return e;
         attr_set[dev] = true;
     }
-    const uint32_t waves = (n + kWaveReqs - 1) / kWaveReqs;
-    const uint32_t grid = (waves + kWaveBlock / 64 - 1) / (kWaveBlock / 64);
-    if (shared)
-        hipLaunchKernelGGL((ajx_wave_eval<true>), dim3(grid), dim3(kWaveBlock), lds, stream, d_sets, d_set_of_req,
-                           d_arena, d_offs, d_lens, n, d_tri, d_err, d_bm, stride, d_rows_out, row_stride,
-                           d_slow_count, d_slow_ids, blob_region, wave_bytes, nbatch, ablate);
+    const uint32_t grid = (n + kLaneBlock - 1) / kLaneBlock;
+#define AJX_LANE_LAUNCH(M, S)                                                                                 \
+    hipLaunchKernelGGL((ajx_lane_eval<M, S>), dim3(grid), dim3(kLaneBlock), lds, stream, d_sets, d_set_of_req,    \
+                       d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, \
+                       stride, blob_region, d_perm)
+    if (mode == 1) AJX_LANE_LAUNCH(1, true);
+    else if (mode == 2) AJX_LANE_LAUNCH(2, true);
+    else if (mode == 3) AJX_LANE_LAUNCH(3, true);
+    else if (mode == 4) AJX_LANE_LAUNCH(4, true);
+    else if (shared)
+        hipLaunchKernelGGL((ajx_lane_eval<0, true>), dim3(grid), dim3(kLaneBlock), lds, stream, d_sets, d_set_of_req,
+                           d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
+                           stride, blob_region, d_perm);
     else
-        hipLaunchKernelGGL((ajx_wave_eval<false>), dim3(grid), dim3(kWaveBlock), lds, stream, d_sets, d_set_of_req,
-                           d_arena, d_offs, d_lens, n, d_tri, d_err, d_bm, stride, d_rows_out, row_stride,
-                           d_slow_count, d_slow_ids, blob_region, wave_bytes, nbatch, ablate);
+        hipLaunchKernelGGL((ajx_lane_eval<0, false>), dim3(grid), dim3(kLaneBlock), lds, stream, d_sets, d_set_of_req,
+                           d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
+                           stride, blob_region, d_perm);
+#undef AJX_LANE_LAUNCH
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (mode == 1 || mode == 2 || mode == 4) return hipSuccess;
     const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
     hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(256), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
                        d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);

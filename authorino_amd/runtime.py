@@ -186,8 +186,8 @@ class Context:
         _check(load_library().authjx_set_exact_scan(self._h, 1 if force else 0), "authjx_set_exact_scan")
 
     def set_kernel_mode(self, mode: int) -> None:
-        """Select the single-pass kernel variant (0 default; others are profiling ablations
-        whose outputs are meaningless). Not part of authjx.h."""
+        """Select the kernel: 0 the single-pass kernel (default), 20 the lane kernel; other
+        values are profiling ablations whose outputs are meaningless. Not part of authjx.h."""
         L = load_library()
         L.authjx_debug_ablate.argtypes = [C.c_void_p, C.c_int]
         _check(L.authjx_debug_ablate(self._h, int(mode)), "authjx_debug_ablate")

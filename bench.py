@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo test of the distributed driver: no GPU, a stand-in step")
     ap.add_argument("--kernel-mode", type=int, default=0,
-                    help="profiling: 0 the wave kernel (default), 6 the round-1 single-pass kernel")
+                    help="0 the single-pass kernel (default), 20 the lane kernel; others: profiling ablations")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 

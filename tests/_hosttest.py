@@ -159,47 +159,45 @@ def eval_fast(hr: "HostRuleset", doc, mis: int = 0):
 _W = None
 
 
-def wave_lib():
-    """tests/native/libajx_wavetest.so: the wave kernel's logic on the host (64-thread wave)."""
+def lane_lib():
+    """tests/native/libajx_lanetest.so: the lane kernel's scanner on the host."""
     global _W
     if _W is None:
         subprocess.run(["make", "-s", "-C", _NATIVE], check=True)
-        L = C.CDLL(os.path.join(_NATIVE, "libajx_wavetest.so"))
+        L = C.CDLL(os.path.join(_NATIVE, "libajx_lanetest.so"))
         L.hw_compile.argtypes = [C.POINTER(_Tree), C.POINTER(C.c_int)]
         L.hw_compile.restype = C.c_void_p
         L.hw_free.argtypes = [C.c_void_p]
-        L.hw_wave_ok.argtypes = [C.c_void_p]
-        L.hw_wave_ok.restype = C.c_int
-        L.hw_eval.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint8, C.POINTER(C.c_uint8),
-                              C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
-                              C.POINTER(C.c_uint32), C.c_uint32]
-        L.hw_eval.restype = C.c_int
+        L.hw_lane_ok.argtypes = [C.c_void_p]
+        L.hw_lane_ok.restype = C.c_int
+        L.hw_eval_lane.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint8, C.POINTER(C.c_uint8),
+                                   C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+        L.hw_eval_lane.restype = C.c_int
         _W = L
     return _W
 
 
-class WaveRuleset:
-    """A ruleset for the wave-kernel harness: eval(doc) -> (tri | -1 exact scan | -2 not
-    eligible, err, per-pattern results, tokens)."""
+class LaneRuleset:
+    """A ruleset for the lane-kernel harness: eval(doc) -> (tri | -1 exact scan | -2 not
+    eligible, err, per-pattern results, capture row)."""
 
     def __init__(self, patterns, nodes, root):
         self.n = len(patterns)
         t, self._keep = make_tree(patterns, nodes, root)
         rc = C.c_int(0)
-        self._h = wave_lib().hw_compile(C.byref(t), C.byref(rc))
+        self._h = lane_lib().hw_compile(C.byref(t), C.byref(rc))
         self.rc = rc.value
-        self.ok = bool(self._h) and bool(wave_lib().hw_wave_ok(self._h))
+        self.ok = bool(self._h) and bool(lane_lib().hw_lane_ok(self._h))
 
     def eval(self, doc, mis=0, fill=0x41):
         d = _b(doc)
         res = (C.c_uint8 * max(self.n, 1))()
         err = C.c_int32(-1)
         row = (C.c_uint64 * 260)()
-        ntok = C.c_uint32(0)
-        toks = (C.c_uint32 * 8192)()
-        t = wave_lib().hw_eval(self._h, d, len(d), mis, fill, res, C.byref(err), row, C.byref(ntok), toks, 8192)
-        return t, err.value, list(res)[: self.n], list(toks)[: ntok.value]
+        nwin = C.c_uint32(0)
+        t = lane_lib().hw_eval_lane(self._h, d, len(d), mis, fill, res, C.byref(err), row, C.byref(nwin))
+        return t, err.value, list(res)[: self.n], list(row)
 
     def __del__(self):
         if getattr(self, "_h", None):
-            wave_lib().hw_free(self._h)
+            lane_lib().hw_free(self._h)

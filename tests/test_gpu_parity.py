@@ -398,3 +398,41 @@ def test_select_from_eval_matches_select_batch(ctx):
     assert (tf[:, -1] == runtime.T).all()
     with pytest.raises(runtime.AuthjxError):  # the rows are the plain forest's now
         ctx.select_from_eval_device(fused, fused.n_patterns - k, A, Of, Ln, got)
+
+
+def test_lane_kernel_matches_oracle(ctx):
+    """The lane kernel (kernel mode 20, ajx_lane.h) on the c2 / c3 workloads, random and
+    malformed documents: the same outputs as the oracle."""
+    import fuzz_util as FU
+    from authorino_amd import workloads as W
+
+    ctx.set_kernel_mode(20)
+    try:
+        for workload, n in (("c2", 50000), ("c3", 20000)):
+            w = W.make(workload, n=n, seed=31)
+            rs = ctx.compile_expression(w.expr)
+            tri, err, bm = ctx.eval_host_arena([rs], w.arena, w.offs, w.lens)
+            assert ctx.last_exact_count() == 0  # every synthetic document took the lane path
+            otri, oerr, obm = _oracle(w.expr, w.arena, w.offs, w.lens)
+            assert np.array_equal(tri, otri) and np.array_equal(err, oerr) and np.array_equal(bm, obm)
+        rng = np.random.default_rng(78)
+        for _ in range(20):
+            pats = FU.rand_patterns(rng, int(rng.integers(1, 10)))
+            nodes, root = FU.chain(len(pats))
+            ors = O.Ruleset(pats, nodes, root)
+            docs = [FU.mutate(rng, d) if rng.random() < 0.3 else d for d in
+                    (FU.rand_doc(rng, ws=False) for _ in range(300))]
+            if any(ors.pattern(p, docs[0]) == O.UNSUPPORTED for p in range(len(pats))):
+                continue
+            rs = ctx.compile(pats, nodes, root)
+            tri, err, bm = ctx.eval_host([rs], docs)
+            lens = np.array([len(d) for d in docs], dtype=np.uint32)
+            offs = np.zeros(len(docs), dtype=np.uint64)
+            offs[1:] = np.cumsum(lens[:-1])
+            arena = np.frombuffer(b"".join(docs) + b"\0", dtype=np.uint8)
+            otri, oerr, obm = O.eval_batch([ors], arena, offs, lens)
+            dec = tri != 3
+            assert np.array_equal(tri[dec], otri[dec])
+            assert np.array_equal(bm[dec], obm[dec])
+    finally:
+        ctx.set_kernel_mode(0)
