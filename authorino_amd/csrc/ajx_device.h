@@ -18,9 +18,17 @@
 #include <stdint.h>
 
 #include "ajx_blob.h"
+#include "ajx_float.h"
 
 #ifndef AJX_HD
 #define AJX_HD __device__ __forceinline__
+#endif
+#ifndef AJX_COLD
+#if defined(__HIPCC__)
+#define AJX_COLD __device__ __attribute__((noinline))  // rare paths kept out of line
+#else
+#define AJX_COLD inline
+#endif
 #endif
 
 namespace ajx {
@@ -160,16 +168,18 @@ AJX_HD uint32_t utf8_put(uint32_t r, uint8_t* o) {
 }
 
 // Canonical number text for Result.String() when Raw is not -?[0-9]+:
-// FormatFloat(ParseFloat(raw), 'f', -1, 64). Exact without float arithmetic for
-// decimals with <= 15 significant digits in the normal range (the shortest round-trip
-// digits of such a double are the decimal's own digits); undecided otherwise.
+// FormatFloat(ParseFloat(raw), 'f', -1, 64). num_canon: exact without float arithmetic
+// for decimals with <= 15 significant digits in the normal range (the shortest
+// round-trip digits of such a double are the decimal's own digits); K_HARD otherwise,
+// which num_canon_exact decides (ajx_float.h). Hex mantissas and '_' separators (never
+// in JSON a Go encoder writes) stay undecided.
 struct NumCanon {
-    enum : uint8_t { K_ZERO, K_DIGITS, K_PINF, K_NINF, K_NAN, K_UNDECIDED };
+    enum : uint8_t { K_ZERO, K_DIGITS, K_PINF, K_NINF, K_NAN, K_UNDECIDED, K_HARD };
     uint8_t kind;
     uint8_t neg;
-    uint8_t nd;     // significant digits (<= 15)
+    uint8_t nd;     // significant digits (<= 17)
     int16_t dp;     // value = 0.D * 10^dp
-    uint8_t dig[16];
+    uint8_t dig[18];
 };
 
 AJX_HD uint8_t lower_c(uint8_t c) { return c | 0x20; }
@@ -239,14 +249,85 @@ AJX_HD void num_canon(const uint8_t* s, uint32_t n, NumCanon* o) {
     }
     if (i != n) { o->kind = NumCanon::K_ZERO; return; }
     if (!seen) { o->kind = NumCanon::K_ZERO; o->neg = neg; return; }  // +-0
-    if (last_nz > 15) { o->kind = NumCanon::K_UNDECIDED; return; }
+    o->neg = neg;
+    if (last_nz > 15) { o->kind = NumCanon::K_HARD; return; }
     int64_t ndp = (int64_t)dp + e;
     if (ndp >= 310) { o->kind = neg ? NumCanon::K_NINF : NumCanon::K_PINF; return; }
-    if (ndp >= 309 || ndp < -306) { o->kind = NumCanon::K_UNDECIDED; return; }
+    if (ndp >= 309 || ndp < -306) { o->kind = NumCanon::K_HARD; return; }
     o->kind = NumCanon::K_DIGITS;
     o->neg = neg;
     o->nd = (uint8_t)last_nz;
     o->dp = (int16_t)ndp;
+}
+
+// num_canon for a K_HARD decimal s[0, n) (syntax already accepted by num_canon):
+// ParseFloat exactly (the first 800 significant digits and a sticky bit, as Go's
+// strconv/decimal keeps them), then the shortest round-trip digits (ajx_float.h).
+AJX_COLD void num_canon_exact(const uint8_t* s, uint32_t n, NumCanon* o) {
+    Big N, t, u;
+    uint32_t i = 0;
+    const bool neg = n > 0 && s[0] == '-';
+    if (n > 0 && (s[0] == '+' || s[0] == '-')) i = 1;
+    bool sawdot = false, seen = false, trunc = false;
+    int dp = 0, nd = 0;
+    uint64_t w19 = 0;
+    uint32_t chunk = 0, cmul = 1;
+    N.set(0);
+    for (; i < n; i++) {
+        const uint8_t c = s[i];
+        if (c == '.') {
+            sawdot = true;
+            continue;
+        }
+        if (c < '0' || c > '9') break;
+        if (!seen && c == '0') {
+            if (sawdot) dp--;
+            continue;
+        }
+        seen = true;
+        if (!sawdot) dp++;
+        if (nd >= 800) {
+            trunc = trunc || c != '0';
+            continue;
+        }
+        if (nd < 19) w19 = w19 * 10 + (uint64_t)(c - '0');
+        nd++;
+        chunk = chunk * 10 + (uint32_t)(c - '0');
+        cmul *= 10;
+        if (cmul == 1000000000u) {
+            N.mul_add(cmul, chunk);
+            if (N.n == 0 && chunk) N.set(chunk);
+            chunk = 0;
+            cmul = 1;
+        }
+    }
+    if (cmul > 1) {
+        N.mul_add(cmul, chunk);
+        if (N.n == 0 && chunk) N.set(chunk);
+    }
+    int64_t e = 0;
+    if (i < n && (s[i] | 0x20) == 'e') {
+        i++;
+        int64_t es = 1;
+        if (s[i] == '+' || s[i] == '-') { es = s[i] == '-' ? -1 : 1; i++; }
+        for (; i < n && s[i] >= '0' && s[i] <= '9'; i++)
+            if (e < 100000) e = e * 10 + (s[i] - '0');
+        e *= es;
+    }
+    o->neg = neg;
+    const int64_t ndp = (int64_t)dp + e;
+    double f;
+    if (ndp > 400) f = f64_from(0x7FF0000000000000ull);
+    else if (ndp < -400) f = 0.0;
+    else f = dec_to_f64(N, nd, (int)ndp - nd, trunc, w19, t, u);
+    const uint64_t fb = f64_bits(f);
+    if (fb == 0) { o->kind = NumCanon::K_ZERO; return; }  // underflow: +-0
+    if (fb >= 0x7FF0000000000000ull) { o->kind = neg ? NumCanon::K_NINF : NumCanon::K_PINF; return; }
+    int ond, odp;
+    f64_shortest(f, o->dig, &ond, &odp, N, t, u);
+    o->kind = NumCanon::K_DIGITS;
+    o->nd = (uint8_t)ond;
+    o->dp = (int16_t)odp;
 }
 
 // Character stream of a Result.String()
@@ -271,12 +352,17 @@ struct StrSrc {
     AJX_HD void init_const(const char* s, uint32_t len) {
         p = (const uint8_t*)s; i = 0; n = len; kind = S_RAW; bn = bi = 0; done = false;
     }
-    // returns false if the number can not be formatted exactly (undecided)
+    // returns false if the number can not be formatted exactly (undecided). EXACT (the
+    // exact scan): K_HARD numbers through num_canon_exact; otherwise they are undecided
+    // here (the single-pass kernels hand such requests to the exact scan)
+    template <bool EXACT = false>
     AJX_HD bool init_num(const uint8_t* s, uint32_t a, uint32_t b) {
         kind = S_NUM; bn = bi = 0; done = false; pos = 0;
         num_canon(s + a, b - a, &num);
+        if (EXACT && num.kind == NumCanon::K_HARD) num_canon_exact(s + a, b - a, &num);
         switch (num.kind) {
-            case NumCanon::K_UNDECIDED: return false;
+            case NumCanon::K_UNDECIDED:
+            case NumCanon::K_HARD: return false;
             case NumCanon::K_ZERO: init_const(num.neg ? "-0" : "0", num.neg ? 2 : 1); return true;
             case NumCanon::K_PINF: init_const("+Inf", 4); return true;
             case NumCanon::K_NINF: init_const("-Inf", 4); return true;
@@ -354,6 +440,7 @@ struct StrSrc {
 };
 
 // Result.String() stream for a value. Returns false when undecided.
+template <bool EXACT = false>
 AJX_HD bool string_of(const uint8_t* d, const ValueRef& v, StrSrc* s) {
     switch (v.type) {
         case T_STRING:
@@ -366,7 +453,7 @@ AJX_HD bool string_of(const uint8_t* d, const ValueRef& v, StrSrc* s) {
             for (; k < v.end; k++)
                 if (d[k] < '0' || d[k] > '9') break;
             if (k == v.end) { s->init_raw(d, v.start, v.end); return true; }
-            return s->init_num(d, v.start, v.end);
+            return s->template init_num<EXACT>(d, v.start, v.end);
         }
         case T_TRUE: s->init_const("true", 4); return true;
         case T_FALSE: s->init_const("false", 5); return true;
@@ -768,6 +855,9 @@ AJX_HD bool dfa_match(const uint8_t* blob, uint32_t dfa_off, StrSrc* s) {
 // ---------------------------------------------------------------------------------
 // Pattern.Matches on a resolved value
 // ---------------------------------------------------------------------------------
+// EXACT: the exact scan's instance (every number decided, ajx_float.h); the
+// single-pass kernels' instance returns V_U for a number it leaves to the exact scan
+template <bool EXACT = false>
 AJX_HD uint8_t eval_pattern(const uint8_t* blob, const Pattern& p, const uint8_t* doc, const ValueRef& v) {
     if (p.state == P_STATIC_E) return V_E;
     if (p.state == P_UNSUPPORTED) return V_U;
@@ -777,7 +867,7 @@ AJX_HD uint8_t eval_pattern(const uint8_t* blob, const Pattern& p, const uint8_t
         case OP_EQ:
         case OP_NEQ: {
             StrSrc s;
-            if (!string_of(doc, v, &s)) return V_U;
+            if (!string_of<EXACT>(doc, v, &s)) return V_U;
             bool eq = stream_equals(&s, lit, p.lit_len);
             return (eq == (p.op == OP_EQ)) ? V_T : V_F;
         }
@@ -789,7 +879,7 @@ AJX_HD uint8_t eval_pattern(const uint8_t* blob, const Pattern& p, const uint8_t
             bool found = false, und = false;
             while (it.next(&e)) {
                 StrSrc s;
-                if (!string_of(doc, e, &s)) { und = true; continue; }
+                if (!string_of<EXACT>(doc, e, &s)) { und = true; continue; }
                 if (stream_equals(&s, lit, p.lit_len)) { found = true; break; }
             }
             if (!found && und) return V_U;
@@ -797,7 +887,7 @@ AJX_HD uint8_t eval_pattern(const uint8_t* blob, const Pattern& p, const uint8_t
         }
         case OP_MATCHES: {
             StrSrc s;
-            if (!string_of(doc, v, &s)) return V_U;
+            if (!string_of<EXACT>(doc, v, &s)) return V_U;
             return dfa_match(blob, p.dfa_off, &s) ? V_T : V_F;
         }
         default: return V_E;

@@ -52,8 +52,8 @@ __device__ __forceinline__ void eval_scan_one(uint32_t r, const uint8_t* const* 
     };
     auto eval = [&](uint32_t p) -> uint8_t {
         const Pattern& pt = pats[p];
-        if (pt.state != P_OK) return eval_pattern(blob, pt, doc, ValueRef{0, 0, T_NULL, 0});
-        return eval_pattern(blob, pt, doc, value_of(p));
+        if (pt.state != P_OK) return eval_pattern<true>(blob, pt, doc, ValueRef{0, 0, T_NULL, 0});
+        return eval_pattern<true>(blob, pt, doc, value_of(p));
     };
 
     uint8_t res[kPatCache];
@@ -194,13 +194,16 @@ __device__ __forceinline__ void fold_outputs(uint32_t r, const uint8_t* blob, co
     }
 }
 
-// stage B for request r on its capture row: patterns, T bitmap, And/Or fold, outputs
-__device__ __forceinline__ void finish_request(uint32_t r, const uint8_t* blob, const uint8_t* d, const uint64_t* row,
+// stage B for request r on its capture row: patterns, T bitmap, And/Or fold, outputs.
+// false (nothing written): a value needs the exact scan (a number only ajx_float.h
+// decides), the caller hands the request over
+__device__ __forceinline__ bool finish_request(uint32_t r, const uint8_t* blob, const uint8_t* d, const uint64_t* row,
                                                uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
                                                uint64_t* __restrict__ out_bm, uint32_t stride) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     uint64_t t[2], u[2];
     patterns_from_row(blob, d, row, t, u);
+    if ((u[0] & ~h->unsupported[0]) | (u[1] & ~h->unsupported[1])) return false;
     if (out_bm) {
         uint64_t* orow = out_bm + (size_t)r * stride;
         orow[0] = t[0];
@@ -209,6 +212,7 @@ __device__ __forceinline__ void finish_request(uint32_t r, const uint8_t* blob, 
     }
     const uint64_t se[2] = {h->static_error[0], h->static_error[1]};
     fold_outputs(r, blob, h, t, u, se, out_tri, out_err);
+    return true;
 }
 
 // Stage A alone (profiling split / ablations): structural scan -> capture rows.
@@ -245,7 +249,7 @@ __global__ __launch_bounds__(kFastBlock) void ajx_patterns(const uint8_t* const*
     if (r >= n) return;
     const uint64_t* row = rows + (size_t)r * row_stride;
     if (row[0] & kRowSlow) return;
-    finish_request(r, blob, arena + offs[r], row, out_tri, out_err, out_bm, stride);
+    (void)finish_request(r, blob, arena + offs[r], row, out_tri, out_err, out_bm, stride);  // (profiling split)
 }
 
 // The single-pass path: stage A then stage B in the same work-item, while the
@@ -274,7 +278,10 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused(con
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
-    finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride);
+    if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
+        row[0] = kRowSlow;
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
+    }
 }
 
 // The single-pass kernel for multi-tenant batches (one ruleset per request through
@@ -302,18 +309,18 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     if (uni) {
         const uint8_t* blob = stage_blob<true>(gblob);
         if (k >= n) return;
-        if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off))) {
+        if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off)) ||
+            !finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
+            row[0] = kRowSlow;
             slow_ids[atomicAdd(slow_count, 1u)] = r;
-            return;
         }
-        finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride);
     } else {
         if (k >= n) return;
-        if (!scan_request<0>(gblob, d, lens[r], row, lane_ring(ring_off))) {
+        if (!scan_request<0>(gblob, d, lens[r], row, lane_ring(ring_off)) ||
+            !finish_request(r, gblob, d, row, out_tri, out_err, out_bm, stride)) {
+            row[0] = kRowSlow;
             slow_ids[atomicAdd(slow_count, 1u)] = r;
-            return;
         }
-        finish_request(r, gblob, d, row, out_tri, out_err, out_bm, stride);
     }
 }
 
@@ -469,7 +476,10 @@ __global__ __launch_bounds__(kLaneBlock, AJX_LANE_WAVES) void ajx_lane_eval(
         out_tri[r] = (uint8_t)row[0];
         return;
     }
-    finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride);
+    if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
+        row[0] = kRowSlow;
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
+    }
 }
 
 hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,

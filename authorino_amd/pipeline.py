@@ -42,7 +42,9 @@ from .response import ResponseConfig, ResponseSelectors, wrap_responses
 
 UNMATCHING_CONDITIONS = "unmatching conditions for config"
 CODE_OK = 0  # rpc.OK
+CODE_UNKNOWN = 2  # rpc.UNKNOWN: the device left the request undecided (AuthResult.undecided)
 CODE_PERMISSION_DENIED = 7  # rpc.PERMISSION_DENIED
+UNDECIDED_MESSAGE = "authjx: undecided on the device"
 
 
 class ConditionsError(Exception):
@@ -92,6 +94,10 @@ class AuthResult:
     message: str = ""
     skipped: bool = False  # AuthConfig-level conditions not met (auth_pipeline.go:454-457)
     denied_by: Optional[str] = None
+    # the device could not decide this request (AUTHJX_UNDECIDED: a pattern compiled as
+    # unsupported, or a hex / '_' number literal in a malformed document); the caller
+    # routes it to its own evaluator. The other requests of the batch are unaffected.
+    undecided: bool = False
     authorization: Dict[str, object] = field(default_factory=dict)
     headers: Dict[str, str] = field(default_factory=dict)      # success: WrapResponses headers
     metadata: Dict[str, object] = field(default_factory=dict)  # success: dynamic metadata
@@ -151,8 +157,6 @@ class AuthPipelineBatch:
             if self._all is None or self._all[0] is not arena:
                 tri, err, _ = self.ctx.eval_host_arena([self._forest], arena, offs, lens, with_bitmap=False)
                 tri = tri.reshape(len(lens), -1)
-                if (tri == runtime.UNDECIDED).any():
-                    raise runtime.AuthjxError("device could not decide a document (AUTHJX_UNDECIDED)")
                 self._all = (arena, tri, err.reshape(len(lens), -1))
             _, tri, err = self._all
             cols = [self._col[id(e)] for e in exprs]
@@ -164,8 +168,6 @@ class AuthPipelineBatch:
         o = np.tile(offs[reqs], k)
         ln = np.tile(lens[reqs], k)
         tri, err, _ = self.ctx.eval_host_arena(sets, arena, o, ln, set_of_req=sor, with_bitmap=False)
-        if (tri == runtime.UNDECIDED).any():
-            raise runtime.AuthjxError("device could not decide a document (AUTHJX_UNDECIDED)")
         return tri.reshape(k, len(reqs)), err.reshape(k, len(reqs)), sets
 
     def evaluate(self, docs: Sequence, producer: Optional[Callable[[int, Dict[str, object]], bytes]] = None
@@ -192,10 +194,22 @@ class AuthPipelineBatch:
         arena, offs, lens = pack(docs)
         self._all = None
         live = np.arange(n)
+
+        def set_aside(tri):  # requests the device left undecided leave the batch
+            nonlocal live
+            und = (tri == runtime.UNDECIDED).any(axis=0)
+            for i in live[und]:
+                results[i].undecided = True
+                results[i].code = CODE_UNKNOWN
+                results[i].message = UNDECIDED_MESSAGE
+            live = live[~und]
+            return ~und
+
         # AuthConfig-level `when` (auth_pipeline.go:454-457): not met -> OK, skipped
         top = self.config.conditions
         if top is not None and n:
             tri, _, _ = self._eval([top], live, arena, offs, lens)
+            tri = tri[:, set_aside(tri)]
             met = tri[0] == runtime.T
             for i in live[~met]:
                 results[i].skipped = True
@@ -211,6 +225,8 @@ class AuthPipelineBatch:
             tri = err = sets = None
             if exprs:
                 tri, err, sets = self._eval(exprs, live, arena, offs, lens)
+                keep = set_aside(tri)
+                tri, err = tri[:, keep], err[:, keep]
             col = {id(e): j for j, e in enumerate(exprs)}
             denied = np.zeros(len(live), dtype=bool)
             for c in level:
@@ -259,6 +275,7 @@ class AuthPipelineBatch:
             met = {}
             if conds:
                 tri, _, _ = self._eval(conds, live, arena_all, offs_all, lens_all)
+                # (an undecided response condition withholds that response only)
                 met = {id(e): tri[j] == runtime.T for j, e in enumerate(conds)}
             for c in level:
                 ok = met[id(c.conditions)] if c.conditions is not None else None

@@ -191,7 +191,7 @@ def result_string(doc: bytes, start: int, length: int, typ: int) -> str:
     if typ == NUMBER:
         if re.fullmatch(rb"-?[0-9]+", raw):
             return raw.decode()
-        return go_format_float(float(raw), "f")
+        return go_format_float(go_parse_float(raw), "f")
     if typ == TRUE:
         return "true"
     if typ == FALSE:
@@ -301,6 +301,27 @@ def _shortest_digits(x: float) -> Tuple[str, int]:
     lead = len(ip + fp) - len((ip + fp).lstrip("0"))
     dp = len(ip) - lead + e
     return digits.rstrip("0") or "0", dp
+
+
+_GO_DEC = re.compile(rb"[+-]?([0-9]+\.?[0-9]*|\.[0-9]+)([eE][+-]?[0-9]+)?")
+_GO_HEX = re.compile(rb"[+-]?0[xX]([0-9a-fA-F]+\.?[0-9a-fA-F]*|\.[0-9a-fA-F]+)[pP][+-]?[0-9]+")
+
+
+def go_parse_float(raw: bytes) -> float:
+    """strconv.ParseFloat(raw, 64) as gjson keeps it (the value even on error: a syntax
+    error gives 0, a range error +-Inf). Python's float() rounds decimal text to
+    nearest-even exactly as Go does; '_' separators (valid in Go only after a base
+    prefix) are not expected in JSON number tokens and read as a syntax error."""
+    if _GO_DEC.fullmatch(raw):
+        return float(raw)
+    if _GO_HEX.fullmatch(raw):
+        return float.fromhex(raw.decode())
+    m = re.fullmatch(rb"([+-]?)(inf|infinity)", raw, re.I)
+    if m:
+        return -math.inf if m.group(1) == b"-" else math.inf
+    if re.fullmatch(rb"nan", raw, re.I):
+        return math.nan
+    return 0.0
 
 
 def go_format_float(x: float, fmt: str) -> str:

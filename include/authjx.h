@@ -70,10 +70,11 @@ extern "C" {
 #define AUTHJX_NODE_OR 2
 
 /* Tri-state result of Expression.Matches: (false,nil)=F, (true,nil)=T, (false,err)=E.
- * UNDECIDED: the device met a value it does not format exactly (a number with more
- * than 15 significant digits / outside the normal range, a hex or underscore number
- * literal); the caller must not take a decision from it. Never produced for
- * documents made by Go's encoding/json with integer or <=15-digit numbers. */
+ * UNDECIDED: the result depends on a pattern compiled as AUTHJX_PAT_UNSUPPORTED, or on
+ * a hex mantissa / '_'-separated number literal (never valid JSON); the caller must not
+ * take a decision from it and routes that request to its own evaluator. Every JSON
+ * number is decided: Go ParseFloat + FormatFloat(f, 'f', -1, 64) run exactly on the
+ * device (ajx_float.h). */
 #define AUTHJX_F 0
 #define AUTHJX_T 1
 #define AUTHJX_E 2

@@ -8,7 +8,13 @@ KEYS = ["a", "b", "c", "ab", "x.y", "0", "1", "ké", "long-key-name", "", "a b",
 STRS = ["", "x", "hello", "a\"b", "back\\slash", "t\tab", "é", "\U0001F600", "<&>", "1", "true", "null",
         "line\nbreak", " ", "-0", "GET", "/api/v1/orders/7"]
 NUMS = ["0", "-0", "1", "-12", "007", "1.5", "1.50", "1e3", "1E-7", "-0.0", "123456789012345", "0.1", "2.5e10",
-        "1e400", "12345678901234567890", "3.14159", "100"]
+        "1e400", "12345678901234567890", "3.14159", "100",
+        # 16-17 significant digits (Go's encoding/json shortest texts), subnormals, the
+        # 1e21 'f'-layout boundary and the float64 ends: decided by the exact scan
+        "0.30000000000000004", "37.77492950000001", "-122.41941550000001", "1.0000000000000002",
+        "9.999999999999999e20", "1e21", "1.2345678901234567e-5", "4.9406564584124654e-324",
+        "2.2250738585072014e-308", "1.7976931348623157e308", "-1.7976931348623157e308", "5e-324",
+        "1.7976931348623159e308", "2.4703282292062328e-324", "1234567890123456.7"]
 
 
 def rand_value(rng, depth):

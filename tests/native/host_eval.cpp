@@ -46,7 +46,7 @@ int ht_eval(void* h, const uint8_t* doc, uint32_t len, uint8_t* res, int32_t* er
             const Selector& s = sels[pats[p].selector];
             v = gj_get(doc, len, comps + s.comp_begin, s.comp_count, lits);
         }
-        res[p] = eval_pattern(blob, pats[p], doc, v);
+        res[p] = eval_pattern<true>(blob, pats[p], doc, v);
     }
     return run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
 }
@@ -81,7 +81,7 @@ int ht_string(const char* path, uint32_t plen, const uint8_t* doc, uint32_t len,
     }
     ValueRef v = gj_get(doc, len, comps.data(), (uint32_t)comps.size(), (const uint8_t*)lits.data());
     StrSrc s;
-    if (!string_of(doc, v, &s)) return -1;
+    if (!string_of<true>(doc, v, &s)) return -1;
     uint32_t k = 0;
     for (int c; (c = s.next()) >= 0;)
         if (k < cap) out[k++] = (uint8_t)c;
@@ -147,6 +147,7 @@ int ht_eval_fast(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_
     if (!ok) return -1;
     uint64_t t[2], u[2];
     patterns_from_row(blob, d, row.data(), t, u);
+    if ((u[0] & ~hd->unsupported[0]) | (u[1] & ~hd->unsupported[1])) return -1;  // a number for the exact scan
     const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
     for (uint32_t p = 0; p < hd->n_patterns; p++) {
         uint64_t bit = 1ull << (p & 63);

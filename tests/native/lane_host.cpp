@@ -80,6 +80,7 @@ int hw_eval_lane(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_
     for (uint32_t s = 0; s <= hd->n_selectors; s++) row_out[s] = row[s];
     uint64_t t[2], u[2];
     patterns_from_row(blob, d, row.data(), t, u);
+    if ((u[0] & ~hd->unsupported[0]) | (u[1] & ~hd->unsupported[1])) return -1;  // a number for the exact scan
     const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
     for (uint32_t p = 0; p < hd->n_patterns; p++) {
         const uint64_t bit = 1ull << (p & 63);
