@@ -13,44 +13,71 @@
 #include "ajx_compiler.h"
 #include "ajx_blob.h"
 #include "ajx_kernels.h"
+#include "ajx_batcher.h"
 
 struct authjx_ruleset {
     int device = 0;
     uint8_t* d_blob = nullptr;
     ajx::CompiledRuleset c;
+    // workspaces (by registry id) whose stream has run a batch over this ruleset:
+    // authjx_free waits for their last batch instead of the whole device
+    std::mutex mu;
+    std::vector<uint64_t> users;
+    void note_use(uint64_t ws_id) {
+        std::lock_guard<std::mutex> lock(mu);
+        if (std::find(users.begin(), users.end(), ws_id) == users.end()) users.push_back(ws_id);
+    }
 };
 
-struct authjx_ctx {
-    int device = 0;
+// Per-stream scratch of a context: every distinct stream a context is called with gets
+// its own set table, slow list, capture rows and request order, so batches on two
+// streams of one context never share a buffer; calls on one stream take its mutex
+// (their kernels are ordered by the stream anyway).
+struct Workspace {
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    std::mutex mu;        // serialises device-side calls on this context (set table)
-    std::mutex batch_mu;  // serialises authjx_eval_batch (owns the staging buffer)
-    // device set table: pointers to ruleset blobs
+    uint64_t id = 0;  // registry id (ruleset users)
+    std::mutex mu;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // ev1: end of the last batch on this stream
     const uint8_t** d_sets = nullptr;
     uint32_t sets_cap = 0;
     std::vector<const uint8_t*> last_sets;
     const uint8_t** h_sets_pinned = nullptr;
-    // staging for authjx_eval_batch (host buffers)
-    uint8_t* d_stage = nullptr;
-    size_t stage_cap = 0;
-    // requests the fast kernel hands to the exact scan
-    uint32_t* d_slow = nullptr;  // [0] = count, [1..] = ids
+    uint32_t* d_slow = nullptr;  // [0] = count, [1..] = ids: requests for the exact scan
     uint32_t slow_cap = 0;
     uint64_t* d_rows = nullptr;  // stage-A capture rows
     size_t rows_cap = 0;         // in u64
     uint32_t* d_perm = nullptr;  // length-bucketed request order (+ 2 x 1024 + 1 u32 histogram)
     uint32_t perm_cap = 0;
-    int len_sort = 1;            // order requests by length class before the single-pass kernel
-    int no_tenant_stage = 0;     // profiling: multi-tenant batches read tables from global memory
-    // the capture rows in d_rows: written by the last single-ruleset, single-pass
-    // evaluation of rows_rs over rows_n requests (nullptr: none usable)
+    // the capture rows in d_rows: written by the last single-ruleset, full evaluation of
+    // rows_rs over rows_n requests on this stream (nullptr: none usable)
     const authjx_ruleset* rows_rs = nullptr;
     uint32_t rows_n = 0, rows_stride = 0;
+    bool ran = false;  // ev0 / ev1 recorded
+};
+
+namespace {
+// live workspaces: id -> (device, end-of-last-batch event); authjx_free looks its
+// ruleset's users up here (an id that is gone belongs to a context already shut down)
+std::mutex g_reg_mu;
+std::vector<std::pair<uint64_t, std::pair<int, hipEvent_t>>> g_reg;
+uint64_t g_next_ws = 1;
+}  // namespace
+
+struct authjx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;  // the context's own stream (host-buffer entry points)
+    std::mutex mu;                 // workspace list and settings
+    std::mutex batch_mu;           // serialises the host-buffer entry points (staging buffer)
+    std::vector<Workspace*> ws;
+    Workspace* last_ws = nullptr;  // of the last device call (last_kernel_ms / last_exact_count)
+    // staging for the host-buffer entry points
+    uint8_t* d_stage = nullptr;
+    size_t stage_cap = 0;
+    int len_sort = 1;         // order requests by length class before the single-pass kernel
+    int no_tenant_stage = 0;  // profiling: multi-tenant batches read tables from global memory
     int force_scan = 0;
     int ablate = 0;  // profiling only: 1/2/3 reduced single-pass variants, 20 the lane kernel,
                      // 21..24 its ablations (ajx_kernels.hip ajx_lane_eval)
-    float last_ms = 0.f;
 };
 
 namespace {
@@ -63,57 +90,122 @@ namespace {
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-int ensure_sets(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets, hipStream_t stream) {
+// the workspace of stream s (created on first use); ctx->mu held by the caller
+Workspace* workspace_of(authjx_ctx* ctx, hipStream_t s) {
+    for (Workspace* w : ctx->ws)
+        if (w->stream == s) return w;
+    Workspace* w = new Workspace();
+    w->stream = s;
+    if (hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->ev1) != hipSuccess) {
+        if (w->ev0) (void)hipEventDestroy(w->ev0);
+        delete w;
+        return nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> lock(g_reg_mu);
+        w->id = g_next_ws++;
+        g_reg.push_back({w->id, {ctx->device, w->ev1}});
+    }
+    ctx->ws.push_back(w);
+    return w;
+}
+
+void destroy_workspace(Workspace* w) {
+    if (w->ran) (void)hipEventSynchronize(w->ev1);
+    {
+        std::lock_guard<std::mutex> lock(g_reg_mu);
+        for (size_t i = 0; i < g_reg.size(); i++)
+            if (g_reg[i].first == w->id) {
+                g_reg.erase(g_reg.begin() + (long)i);
+                break;
+            }
+    }
+    if (w->d_sets) (void)hipFree(w->d_sets);
+    if (w->h_sets_pinned) (void)hipHostFree(w->h_sets_pinned);
+    if (w->d_slow) (void)hipFree(w->d_slow);
+    if (w->d_rows) (void)hipFree(w->d_rows);
+    if (w->d_perm) (void)hipFree(w->d_perm);
+    if (w->ev0) (void)hipEventDestroy(w->ev0);
+    if (w->ev1) (void)hipEventDestroy(w->ev1);
+    delete w;
+}
+
+int ensure_sets(Workspace* w, int device, const authjx_ruleset* const* sets, uint32_t n_sets) {
     std::vector<const uint8_t*> ptrs(n_sets);
     for (uint32_t i = 0; i < n_sets; i++) {
-        if (!sets[i] || sets[i]->device != ctx->device) return AUTHJX_EINVAL;
+        if (!sets[i] || sets[i]->device != device) return AUTHJX_EINVAL;
         ptrs[i] = sets[i]->d_blob;
     }
-    if (ptrs == ctx->last_sets) return AUTHJX_OK;
-    if (n_sets > ctx->sets_cap) {
-        if (ctx->d_sets) (void)hipFree(ctx->d_sets);
-        if (ctx->h_sets_pinned) (void)hipHostFree(ctx->h_sets_pinned);
-        ctx->d_sets = nullptr;
-        ctx->h_sets_pinned = nullptr;
+    if (ptrs == w->last_sets) return AUTHJX_OK;
+    // the table and its pinned source may still be read by this stream's previous batch
+    HIP_OK(hipStreamSynchronize(w->stream));
+    if (n_sets > w->sets_cap) {
+        if (w->d_sets) (void)hipFree(w->d_sets);
+        if (w->h_sets_pinned) (void)hipHostFree(w->h_sets_pinned);
+        w->d_sets = nullptr;
+        w->h_sets_pinned = nullptr;
+        w->sets_cap = 0;
         uint32_t cap = n_sets < 64 ? 64 : n_sets;
-        HIP_OK(hipMalloc(&ctx->d_sets, cap * sizeof(uint8_t*)));
-        HIP_OK(hipHostMalloc(&ctx->h_sets_pinned, cap * sizeof(uint8_t*), hipHostMallocDefault));
-        ctx->sets_cap = cap;
+        HIP_OK(hipMalloc(&w->d_sets, cap * sizeof(uint8_t*)));
+        HIP_OK(hipHostMalloc(&w->h_sets_pinned, cap * sizeof(uint8_t*), hipHostMallocDefault));
+        w->sets_cap = cap;
     }
-    // the pinned table may still be read by an in-flight copy of the previous batch
-    HIP_OK(hipStreamSynchronize(stream));
-    std::memcpy(ctx->h_sets_pinned, ptrs.data(), n_sets * sizeof(uint8_t*));
-    HIP_OK(hipMemcpyAsync(ctx->d_sets, ctx->h_sets_pinned, n_sets * sizeof(uint8_t*), hipMemcpyHostToDevice, stream));
-    ctx->last_sets = ptrs;
+    std::memcpy(w->h_sets_pinned, ptrs.data(), n_sets * sizeof(uint8_t*));
+    HIP_OK(hipMemcpyAsync(w->d_sets, w->h_sets_pinned, n_sets * sizeof(uint8_t*), hipMemcpyHostToDevice, w->stream));
+    w->last_sets = ptrs;
     return AUTHJX_OK;
 }
 
-// capture rows, slow list and request order for a batch of n on stream s (grown when
-// needed: no batch in flight on this context may still use the old buffers)
-int ensure_work(authjx_ctx* ctx, uint32_t n, uint32_t row_stride, hipStream_t s) {
-    if (n <= ctx->slow_cap && n <= ctx->perm_cap && (size_t)n * row_stride <= ctx->rows_cap) return AUTHJX_OK;
-    HIP_OK(hipStreamSynchronize(s));
-    if (n > ctx->slow_cap) {
-        if (ctx->d_slow) (void)hipFree(ctx->d_slow);
-        ctx->d_slow = nullptr;
-        ctx->slow_cap = 0;
-        HIP_OK(hipMalloc(&ctx->d_slow, ((size_t)n + 1) * sizeof(uint32_t)));
-        ctx->slow_cap = n;
+// capture rows, slow list and request order for a batch of n (grown when needed, after
+// this stream's earlier batches are done with the old buffers)
+int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
+    if (n <= w->slow_cap && n <= w->perm_cap && (size_t)n * row_stride <= w->rows_cap) return AUTHJX_OK;
+    HIP_OK(hipStreamSynchronize(w->stream));
+    w->rows_rs = nullptr;
+    if (n > w->slow_cap) {
+        if (w->d_slow) (void)hipFree(w->d_slow);
+        w->d_slow = nullptr;
+        w->slow_cap = 0;
+        HIP_OK(hipMalloc(&w->d_slow, ((size_t)n + 1) * sizeof(uint32_t)));
+        w->slow_cap = n;
     }
-    if (n > ctx->perm_cap) {
-        if (ctx->d_perm) (void)hipFree(ctx->d_perm);
-        ctx->d_perm = nullptr;
-        ctx->perm_cap = 0;
-        HIP_OK(hipMalloc(&ctx->d_perm, ((size_t)n + 4096) * sizeof(uint32_t)));
-        ctx->perm_cap = n;
+    if (n > w->perm_cap) {
+        if (w->d_perm) (void)hipFree(w->d_perm);
+        w->d_perm = nullptr;
+        w->perm_cap = 0;
+        HIP_OK(hipMalloc(&w->d_perm, ((size_t)n + 4096) * sizeof(uint32_t)));
+        w->perm_cap = n;
     }
-    if ((size_t)n * row_stride > ctx->rows_cap) {
-        if (ctx->d_rows) (void)hipFree(ctx->d_rows);
-        ctx->d_rows = nullptr;
-        ctx->rows_cap = 0;
-        HIP_OK(hipMalloc(&ctx->d_rows, (size_t)n * row_stride * sizeof(uint64_t)));
-        ctx->rows_cap = (size_t)n * row_stride;
+    if ((size_t)n * row_stride > w->rows_cap) {
+        if (w->d_rows) (void)hipFree(w->d_rows);
+        w->d_rows = nullptr;
+        w->rows_cap = 0;
+        HIP_OK(hipMalloc(&w->d_rows, (size_t)n * row_stride * sizeof(uint64_t)));
+        w->rows_cap = (size_t)n * row_stride;
     }
+    return AUTHJX_OK;
+}
+
+// a device call's workspace, locked: ctx->mu only while the workspace is looked up
+struct WsLock {
+    Workspace* w = nullptr;
+    std::unique_lock<std::mutex> lock;
+    WsLock(authjx_ctx* ctx, void* stream) {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        w = workspace_of(ctx, stream ? (hipStream_t)stream : ctx->stream);
+        if (w) {
+            lock = std::unique_lock<std::mutex>(w->mu);
+            ctx->last_ws = w;
+        }
+    }
+};
+
+// after the launches of a batch: ev1 marks its end on the stream; the rulesets record
+// this workspace as a user
+int batch_done(Workspace* w, const authjx_ruleset* const* sets, uint32_t n_sets) {
+    HIP_OK(hipEventRecord(w->ev1, w->stream));
+    w->ran = true;
+    for (uint32_t i = 0; i < n_sets; i++) const_cast<authjx_ruleset*>(sets[i])->note_use(w->id);
     return AUTHJX_OK;
 }
 
@@ -135,8 +227,7 @@ int authjx_init(int device, authjx_ctx** out) {
     HIP_OK(hipSetDevice(device));
     authjx_ctx* c = new authjx_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return AUTHJX_EDEVICE;
     }
@@ -148,14 +239,8 @@ void authjx_shutdown(authjx_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->d_sets) (void)hipFree(ctx->d_sets);
-    if (ctx->h_sets_pinned) (void)hipHostFree(ctx->h_sets_pinned);
+    for (Workspace* w : ctx->ws) destroy_workspace(w);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
-    if (ctx->d_slow) (void)hipFree(ctx->d_slow);
-    if (ctx->d_rows) (void)hipFree(ctx->d_rows);
-    if (ctx->d_perm) (void)hipFree(ctx->d_perm);
-    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
-    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -214,7 +299,15 @@ void authjx_free(authjx_ruleset* rs) {
     if (!rs) return;
     if (rs->d_blob) {
         (void)hipSetDevice(rs->device);
-        (void)hipDeviceSynchronize();  // no batch may still read the blob
+        // wait for the last batch of every stream that used this ruleset (not the device:
+        // other streams' batches and other work go on)
+        {
+            std::lock_guard<std::mutex> lock(rs->mu);
+            std::lock_guard<std::mutex> reg(g_reg_mu);
+            for (uint64_t id : rs->users)
+                for (const auto& e : g_reg)
+                    if (e.first == id) (void)hipEventSynchronize(e.second.second);
+        }
         (void)hipFree(rs->d_blob);
     }
     delete rs;
@@ -247,64 +340,71 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     }
     const uint32_t row_stride = 1 + max_sel;
     if (d_out_bitmap && bitmap_stride_words < need_words) return AUTHJX_EINVAL;
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    int force_scan, ablate, len_sort, no_tenant_stage;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        force_scan = ctx->force_scan;
+        ablate = ctx->ablate;
+        len_sort = ctx->len_sort;
+        no_tenant_stage = ctx->no_tenant_stage;
+    }
+    WsLock wl(ctx, stream);
+    Workspace* w = wl.w;
+    if (!w) return AUTHJX_EDEVICE;
+    hipStream_t s = w->stream;
     HIP_OK(hipSetDevice(ctx->device));
-    int rc = ensure_sets(ctx, sets, n_sets, s);
+    int rc = ensure_sets(w, ctx->device, sets, n_sets);
     if (rc != AUTHJX_OK) return rc;
-    if (!ctx->force_scan) {
-        rc = ensure_work(ctx, n, row_stride, s);
+    if (!force_scan) {
+        rc = ensure_work(w, n, row_stride);
         if (rc != AUTHJX_OK) return rc;
     }
-    HIP_OK(hipEventRecord(ctx->ev0, s));
+    HIP_OK(hipEventRecord(w->ev0, s));
     // kernel: the single-pass kernel (default; ajx_scan_fused); ablate 20 the lane
     // kernel (21..24 its ablations), 1..3 single-pass ablations
-    bool fast_tables = !ctx->force_scan;
+    bool fast_tables = !force_scan;
     for (uint32_t i = 0; i < n_sets && fast_tables; i++)
         fast_tables = (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagFastOk) != 0;
-    const bool lane = fast_tables && ctx->ablate >= 20;
+    const bool lane = fast_tables && ablate >= 20;
     // capture rows kept for authjx_select_from_eval_device: one ruleset, a full kernel
-    const bool full = ctx->ablate == 0 || ctx->ablate == 20;
-    const bool keep_rows = !ctx->force_scan && n_sets == 1 && full;
-    ctx->rows_rs = keep_rows ? sets[0] : nullptr;
-    ctx->rows_n = n;
-    ctx->rows_stride = row_stride;
+    const bool full = ablate == 0 || ablate == 20;
+    const bool keep_rows = !force_scan && n_sets == 1 && full;
+    w->rows_rs = keep_rows ? sets[0] : nullptr;
+    w->rows_n = n;
+    w->rows_stride = row_stride;
     size_t max_blob = 0;
     for (uint32_t i = 0; i < n_sets; i++) max_blob = std::max(max_blob, sets[i]->c.blob.size());
-    if (ctx->force_scan) {
-        HIP_OK(ajx::launch_eval_scan(ctx->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
+    if (force_scan) {
+        HIP_OK(ajx::launch_eval_scan(w->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
     } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
         // caller's bucketing by AuthConfig), a full kernel, batches worth sorting
         const uint32_t* perm = nullptr;
-        if (ctx->len_sort && (n_sets == 1 || ctx->len_sort > 1) && full && n >= 4096) {
-            HIP_OK(ajx::launch_len_order(d_lens, n, ctx->d_perm + n, ctx->d_perm, s));
-            perm = ctx->d_perm;
+        if (len_sort && (n_sets == 1 || len_sort > 1) && full && n >= 4096) {
+            HIP_OK(ajx::launch_len_order(d_lens, n, w->d_perm + n, w->d_perm, s));
+            perm = w->d_perm;
         }
         if (lane) {
             const uint32_t stage_bytes =
                 n_sets == 1 && max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u;
-            HIP_OK(ajx::launch_eval_lane(ctx->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
+            HIP_OK(ajx::launch_eval_lane(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                          d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
-                                         ctx->d_rows, row_stride, ctx->d_slow, ctx->d_slow + 1, s,
-                                         ctx->ablate - 20, perm));
+                                         w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s, ablate - 20, perm));
         } else {
             // uniform batch: the blob staged once per workgroup; multi-tenant batch: the
             // largest blob, for workgroups whose requests share one ruleset
             // (ajx_scan_fused_tenant)
             const uint32_t stage_bytes =
                 n_sets == 1 ? (max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u)
-                            : (!ctx->no_tenant_stage && max_blob <= ajx::kMaxTenantStageBytes ? (uint32_t)max_blob
-                                                                                              : 0u);
-            HIP_OK(ajx::launch_eval_fast(ctx->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
+                            : (!no_tenant_stage && max_blob <= ajx::kMaxTenantStageBytes ? (uint32_t)max_blob : 0u);
+            HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                          d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
-                                         ctx->d_rows, row_stride, ctx->d_slow, ctx->d_slow + 1, s,
-                                         ctx->ablate < 20 ? ctx->ablate : 0, perm));
+                                         w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
+                                         ablate < 20 ? ablate : 0, perm));
         }
     }
-    HIP_OK(hipEventRecord(ctx->ev1, s));
-    return AUTHJX_OK;
+    return batch_done(w, sets, n_sets);
 }
 
 static_assert(sizeof(authjx_value) == 12, "authjx_value is three u32 words on the device");
@@ -323,25 +423,33 @@ int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* set
         if (sets[i]->c.n_selectors > max_sel) max_sel = sets[i]->c.n_selectors;
     }
     const uint32_t row_stride = 1 + max_sel;
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    int force_scan, len_sort;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        force_scan = ctx->force_scan;
+        len_sort = ctx->len_sort;
+    }
+    WsLock wl(ctx, stream);
+    Workspace* w = wl.w;
+    if (!w) return AUTHJX_EDEVICE;
+    hipStream_t s = w->stream;
     HIP_OK(hipSetDevice(ctx->device));
-    int rc = ensure_sets(ctx, sets, n_sets, s);
+    int rc = ensure_sets(w, ctx->device, sets, n_sets);
     if (rc != AUTHJX_OK) return rc;
-    const bool exact = ctx->force_scan != 0;  // the exact Get per selector (cross-check)
-    ctx->rows_rs = nullptr;  // (the rows are rewritten for this ruleset)
-    if (!exact && (rc = ensure_work(ctx, n, row_stride, s)) != AUTHJX_OK) return rc;
+    const bool exact = force_scan != 0;  // the exact Get per selector (cross-check)
+    w->rows_rs = nullptr;  // (the rows are rewritten for this ruleset)
+    if (!exact && (rc = ensure_work(w, n, row_stride)) != AUTHJX_OK) return rc;
     const uint32_t* perm = nullptr;
-    if (!exact && ctx->len_sort && n_sets == 1 && n >= 4096) {
-        HIP_OK(ajx::launch_len_order(d_lens, n, ctx->d_perm + n, ctx->d_perm, s));
-        perm = ctx->d_perm;
+    if (!exact && len_sort && n_sets == 1 && n >= 4096) {
+        HIP_OK(ajx::launch_len_order(d_lens, n, w->d_perm + n, w->d_perm, s));
+        perm = w->d_perm;
     }
     const uint32_t shared_bytes =
         (n_sets == 1 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes) ? (uint32_t)sets[0]->c.blob.size() : 0u;
-    HIP_OK(ajx::launch_select(ctx->d_sets, d_set_of_req, shared_bytes, d_arena, d_offs, d_lens, n,
+    HIP_OK(ajx::launch_select(w->d_sets, d_set_of_req, shared_bytes, d_arena, d_offs, d_lens, n,
                               reinterpret_cast<uint32_t*>(d_out_values), values_stride,
-                              exact ? nullptr : ctx->d_rows, row_stride, ctx->d_slow, ctx->d_slow + 1, perm, s));
-    return AUTHJX_OK;
+                              exact ? nullptr : w->d_rows, row_stride, w->d_slow, w->d_slow + 1, perm, s));
+    return batch_done(w, sets, n_sets);
 }
 
 int authjx_select_from_eval_device(authjx_ctx* ctx, const authjx_ruleset* rs, uint32_t first_pattern,
@@ -350,17 +458,20 @@ int authjx_select_from_eval_device(authjx_ctx* ctx, const authjx_ruleset* rs, ui
     if (!ctx || !rs || values_stride == 0 || (n && (!d_arena || !d_offs || !d_lens || !d_out_values)))
         return AUTHJX_EINVAL;
     if (first_pattern + values_stride > rs->c.n_patterns) return AUTHJX_EINVAL;
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    // the rows must be the last evaluation's, of this ruleset, over this many requests
-    if (ctx->rows_rs != rs || ctx->rows_n != n) return AUTHJX_EINVAL;
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    WsLock wl(ctx, stream);
+    Workspace* w = wl.w;
+    if (!w) return AUTHJX_EDEVICE;
+    // the rows must be this stream's last evaluation's, of this ruleset, over this many
+    // requests
+    if (w->rows_rs != rs || w->rows_n != n) return AUTHJX_EINVAL;
+    hipStream_t s = w->stream;
     HIP_OK(hipSetDevice(ctx->device));
     const authjx_ruleset* one[1] = {rs};
-    int rc = ensure_sets(ctx, one, 1, s);
+    int rc = ensure_sets(w, ctx->device, one, 1);
     if (rc != AUTHJX_OK) return rc;
-    HIP_OK(ajx::launch_select_rows(ctx->d_sets, d_arena, d_offs, d_lens, n, reinterpret_cast<uint32_t*>(d_out_values),
-                                   values_stride, ctx->d_rows, ctx->rows_stride, first_pattern, s));
-    return AUTHJX_OK;
+    HIP_OK(ajx::launch_select_rows(w->d_sets, d_arena, d_offs, d_lens, n, reinterpret_cast<uint32_t*>(d_out_values),
+                                   values_stride, w->d_rows, w->rows_stride, first_pattern, s));
+    return batch_done(w, one, 1);
 }
 
 int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
@@ -369,7 +480,7 @@ int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint
                         uint32_t values_stride) {
     if (!ctx || (n && (!arena || !offs || !lens || !out_values))) return AUTHJX_EINVAL;
     for (uint32_t r = 0; r < n; r++)
-        if (offs[r] + lens[r] > arena_len) return AUTHJX_EINVAL;
+        if (offs[r] + lens[r] > arena_len || (set_of_req && set_of_req[r] >= n_sets)) return AUTHJX_EINVAL;
     const bool with_sor = set_of_req != nullptr;
     const size_t o_offs = round_up(arena_len, 256);
     const size_t o_lens = round_up(o_offs + (size_t)n * 8, 256);
@@ -379,7 +490,6 @@ int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint
     const size_t total = round_up(o_out + out_bytes, 256);
     std::lock_guard<std::mutex> batch_lock(ctx->batch_mu);
     {
-        std::lock_guard<std::mutex> lock(ctx->mu);
         HIP_OK(hipSetDevice(ctx->device));
         if (total > ctx->stage_cap) {
             HIP_OK(hipStreamSynchronize(ctx->stream));
@@ -401,7 +511,6 @@ int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint
                                         (const uint64_t*)(b + o_offs), (const uint32_t*)(b + o_lens), n,
                                         (authjx_value*)(b + o_out), values_stride, nullptr);
     if (rc != AUTHJX_OK) return rc;
-    std::lock_guard<std::mutex> lock(ctx->mu);
     HIP_OK(hipMemcpyAsync(out_values, b + o_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_OK(hipStreamSynchronize(ctx->stream));
     return AUTHJX_OK;
@@ -444,20 +553,35 @@ int authjx_set_exact_scan(authjx_ctx* ctx, int force) {
 
 int64_t authjx_last_exact_count(authjx_ctx* ctx) {
     if (!ctx) return AUTHJX_EINVAL;
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    if (ctx->force_scan || !ctx->d_slow) return -1;
+    Workspace* w;
+    int force_scan;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        w = ctx->last_ws;
+        force_scan = ctx->force_scan;
+    }
+    if (force_scan || !w) return -1;
+    std::lock_guard<std::mutex> lock(w->mu);
+    if (!w->d_slow || !w->ran) return -1;
     uint32_t c = 0;
-    if (hipSetDevice(ctx->device) != hipSuccess || hipEventSynchronize(ctx->ev1) != hipSuccess ||
-        hipMemcpy(&c, ctx->d_slow, sizeof c, hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipSetDevice(ctx->device) != hipSuccess || hipEventSynchronize(w->ev1) != hipSuccess ||
+        hipMemcpy(&c, w->d_slow, sizeof c, hipMemcpyDeviceToHost) != hipSuccess)
         return AUTHJX_EDEVICE;
     return (int64_t)c;
 }
 
 float authjx_last_kernel_ms(authjx_ctx* ctx) {
     if (!ctx) return 0.f;
+    Workspace* w;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        w = ctx->last_ws;
+    }
+    if (!w) return 0.f;
+    std::lock_guard<std::mutex> lock(w->mu);
     float ms = 0.f;
-    if (hipEventSynchronize(ctx->ev1) != hipSuccess) return 0.f;
-    if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return 0.f;
+    if (!w->ran || hipEventSynchronize(w->ev1) != hipSuccess) return 0.f;
+    if (hipEventElapsedTime(&ms, w->ev0, w->ev1) != hipSuccess) return 0.f;
     return ms;
 }
 
@@ -467,7 +591,7 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
                       uint64_t* out_bitmap, uint32_t bitmap_stride_words) {
     if (!ctx || (n && (!arena || !offs || !lens || !out_tristate))) return AUTHJX_EINVAL;
     for (uint32_t r = 0; r < n; r++)
-        if (offs[r] + lens[r] > arena_len) return AUTHJX_EINVAL;
+        if (offs[r] + lens[r] > arena_len || (set_of_req && set_of_req[r] >= n_sets)) return AUTHJX_EINVAL;
     const bool with_sor = set_of_req != nullptr;
     if (!sets || n_sets == 0 || !sets[0]) return AUTHJX_EINVAL;
     const size_t nt = sets[0]->c.n_trees;  // results per request
@@ -481,9 +605,9 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
     size_t total = round_up(o_bm + (out_bitmap ? (size_t)n * bitmap_stride_words * 8 : 0), 256);
     std::lock_guard<std::mutex> batch_lock(ctx->batch_mu);
     {
-        std::lock_guard<std::mutex> lock(ctx->mu);
         HIP_OK(hipSetDevice(ctx->device));
         if (total > ctx->stage_cap) {
+            HIP_OK(hipStreamSynchronize(ctx->stream));
             if (ctx->d_stage) (void)hipFree(ctx->d_stage);
             ctx->d_stage = nullptr;
             ctx->stage_cap = 0;
@@ -503,13 +627,156 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
                                       b + o_tri, out_err_idx ? (int32_t*)(b + o_err) : nullptr,
                                       out_bitmap ? (uint64_t*)(b + o_bm) : nullptr, bitmap_stride_words, nullptr);
     if (rc != AUTHJX_OK) return rc;
-    std::lock_guard<std::mutex> lock(ctx->mu);
     hipStream_t s = ctx->stream;
     HIP_OK(hipMemcpyAsync(out_tristate, b + o_tri, (size_t)n * nt, hipMemcpyDeviceToHost, s));
     if (out_err_idx) HIP_OK(hipMemcpyAsync(out_err_idx, b + o_err, (size_t)n * nt * 4, hipMemcpyDeviceToHost, s));
     if (out_bitmap)
         HIP_OK(hipMemcpyAsync(out_bitmap, b + o_bm, (size_t)n * bitmap_stride_words * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
+    return AUTHJX_OK;
+}
+
+// ---- micro-batcher ------------------------------------------------------------------
+
+}  // extern "C"
+
+struct authjx_batcher {
+    authjx_ctx* ctx = nullptr;
+    hipStream_t stream = nullptr;  // its own stream: its own workspace in ctx
+    uint8_t* h_buf = nullptr;      // pinned staging: arena | offs | lens | set_of_req | outputs
+    size_t h_cap = 0;
+    uint8_t* d_buf = nullptr;
+    size_t d_cap = 0;
+    ajx::BatchCore* core = nullptr;
+
+    // one batch (ordered by ruleset): pack, one launch, outputs back (worker thread only)
+    int evaluate(std::vector<ajx::BatchReq*>& reqs) {
+        const uint32_t n = (uint32_t)reqs.size(), nt = reqs[0]->n_out;
+        std::vector<const authjx_ruleset*> sets;
+        std::vector<uint32_t> sor(n);
+        size_t arena_len = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const authjx_ruleset* rs = (const authjx_ruleset*)reqs[i]->rs;
+            if (sets.empty() || sets.back() != rs) sets.push_back(rs);
+            sor[i] = (uint32_t)sets.size() - 1;
+            arena_len += reqs[i]->len;
+        }
+        const size_t o_offs = round_up(arena_len + 1, 256);
+        const size_t o_lens = round_up(o_offs + (size_t)n * 8, 256);
+        const size_t o_sor = round_up(o_lens + (size_t)n * 4, 256);
+        const size_t o_tri = round_up(o_sor + (size_t)n * 4, 256);
+        const size_t o_err = round_up(o_tri + (size_t)n * nt, 256);
+        const size_t total = round_up(o_err + (size_t)n * nt * 4, 256);
+        HIP_OK(hipSetDevice(ctx->device));
+        if (total > h_cap) {
+            if (h_buf) (void)hipHostFree(h_buf);
+            h_buf = nullptr;
+            h_cap = 0;
+            HIP_OK(hipHostMalloc(&h_buf, total, hipHostMallocDefault));
+            h_cap = total;
+        }
+        if (total > d_cap) {
+            if (d_buf) (void)hipFree(d_buf);
+            d_buf = nullptr;
+            d_cap = 0;
+            HIP_OK(hipMalloc(&d_buf, total));
+            d_cap = total;
+        }
+        uint64_t* offs = (uint64_t*)(h_buf + o_offs);
+        uint32_t* lens = (uint32_t*)(h_buf + o_lens);
+        size_t at = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            if (reqs[i]->len) std::memcpy(h_buf + at, reqs[i]->doc, reqs[i]->len);
+            offs[i] = at;
+            lens[i] = (uint32_t)reqs[i]->len;
+            at += reqs[i]->len;
+        }
+        h_buf[at] = 0;
+        std::memcpy(h_buf + o_sor, sor.data(), (size_t)n * 4);
+        HIP_OK(hipMemcpyAsync(d_buf, h_buf, o_tri, hipMemcpyHostToDevice, stream));
+        const int rc = authjx_eval_batch_device(ctx, sets.data(), (uint32_t)sets.size(),
+                                                (const uint32_t*)(d_buf + o_sor), d_buf,
+                                                (const uint64_t*)(d_buf + o_offs), (const uint32_t*)(d_buf + o_lens),
+                                                n, d_buf + o_tri, (int32_t*)(d_buf + o_err), nullptr, 0, stream);
+        if (rc != AUTHJX_OK) return rc;
+        HIP_OK(hipMemcpyAsync(h_buf + o_tri, d_buf + o_tri, total - o_tri, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipStreamSynchronize(stream));
+        const uint8_t* tri = h_buf + o_tri;
+        const int32_t* err = (const int32_t*)(h_buf + o_err);
+        for (uint32_t i = 0; i < n; i++) {
+            for (uint32_t k = 0; k < nt; k++) {
+                reqs[i]->out_tri[k] = tri[(size_t)i * nt + k];
+                if (reqs[i]->out_err) reqs[i]->out_err[k] = err[(size_t)i * nt + k];
+            }
+        }
+        return AUTHJX_OK;
+    }
+};
+
+extern "C" {
+
+int authjx_batcher_create(authjx_ctx* ctx, uint32_t max_batch, uint32_t window_us, uint32_t queue_cap,
+                          authjx_batcher** out) {
+    if (!ctx || !out || max_batch == 0) return AUTHJX_EINVAL;
+    *out = nullptr;
+    HIP_OK(hipSetDevice(ctx->device));
+    authjx_batcher* b = new authjx_batcher();
+    b->ctx = ctx;
+    if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete b;
+        return AUTHJX_EDEVICE;
+    }
+    b->core = new ajx::BatchCore(max_batch, (uint64_t)window_us * 1000ull, queue_cap ? queue_cap : 4 * max_batch,
+                                 [b](std::vector<ajx::BatchReq*>& reqs) { return b->evaluate(reqs); });
+    *out = b;
+    return AUTHJX_OK;
+}
+
+void authjx_batcher_destroy(authjx_batcher* b) {
+    if (!b) return;
+    delete b->core;  // evaluates what is queued, joins the worker
+    (void)hipSetDevice(b->ctx->device);
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    if (b->h_buf) (void)hipHostFree(b->h_buf);
+    if (b->d_buf) (void)hipFree(b->d_buf);
+    {
+        // the context keeps the stream's workspace until shutdown; the stream goes now
+        std::lock_guard<std::mutex> g(b->ctx->mu);
+        for (size_t i = 0; i < b->ctx->ws.size(); i++)
+            if (b->ctx->ws[i]->stream == b->stream) {
+                if (b->ctx->last_ws == b->ctx->ws[i]) b->ctx->last_ws = nullptr;
+                destroy_workspace(b->ctx->ws[i]);
+                b->ctx->ws.erase(b->ctx->ws.begin() + (long)i);
+                break;
+            }
+    }
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;
+}
+
+int authjx_batcher_eval(authjx_batcher* b, const authjx_ruleset* rs, const uint8_t* doc, size_t len,
+                        uint64_t timeout_us, uint8_t* out_tristate, int32_t* out_err_idx) {
+    if (!b || !rs || (!doc && len) || !out_tristate || len >= (1ull << 32)) return AUTHJX_EINVAL;
+    if (rs->device != b->ctx->device) return AUTHJX_EINVAL;
+    ajx::BatchReq r;
+    r.rs = rs;
+    r.n_out = rs->c.n_trees;
+    r.doc = doc;
+    r.len = len;
+    r.deadline_ns = timeout_us ? ajx::mono_ns() + timeout_us * 1000ull : 0;
+    r.out_tri = out_tristate;
+    r.out_err = out_err_idx;
+    return b->core->submit(r);
+}
+
+int authjx_batcher_stats(authjx_batcher* b, uint64_t* batches, uint64_t* requests, uint64_t* expired,
+                         uint64_t* max_batch_seen) {
+    if (!b) return AUTHJX_EINVAL;
+    const ajx::BatchStats st = b->core->stats();
+    if (batches) *batches = st.batches;
+    if (requests) *requests = st.requests;
+    if (expired) *expired = st.expired;
+    if (max_batch_seen) *max_batch_seen = st.max_batch_seen;
     return AUTHJX_OK;
 }
 

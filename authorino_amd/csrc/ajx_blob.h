@@ -87,7 +87,7 @@ struct RuneRange {
 // moves from a node to one of its children.
 constexpr uint32_t kFastMaxPatterns = 128;
 constexpr uint32_t kFastMaxNodes = 255;
-constexpr uint32_t kFastMaxSelectors = 64;
+constexpr uint32_t kFastMaxSelectors = 63;  // found bits 0..62 (bit 63 of the row header is kRowSlow)
 constexpr uint8_t kNoNode = 0xFF;
 
 struct TrieNode {

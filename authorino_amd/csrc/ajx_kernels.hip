@@ -13,11 +13,28 @@
 //                then the patterns and the fold. Exact for arbitrary input bytes.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "ajx_fast.h"
 #include "ajx_lane.h"
 #include "ajx_kernels.h"
 
 namespace ajx {
+
+// The dynamic-LDS ceiling of a group of kernels is set once per device (the attribute
+// belongs to that device's code object); any thread may launch first, so the per-device
+// bits are atomic (setting an attribute twice is harmless).
+template <class F>
+static hipError_t attr_once(std::atomic<uint64_t>& done, F set) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = dev >= 0 && dev < 64 ? 1ull << dev : 0ull;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+    if ((e = set()) != hipSuccess) return e;
+    done.fetch_or(bit, std::memory_order_acq_rel);
+    return hipSuccess;
+}
 
 constexpr int kSelCache = 32;  // resolved selector values kept per request
 constexpr int kPatCache = 64;  // pattern results kept per request for the fold
@@ -494,21 +511,21 @@ hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_
     if (lds > 160 * 1024 || (mode != 0 && !shared)) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    int dev = 0;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-    static bool attr_set[64] = {};
-    if (dev >= 0 && dev < 64 && !attr_set[dev]) {
+    static std::atomic<uint64_t> attr_done{0};
+    e = attr_once(attr_done, [] {
         const void* ks[] = {reinterpret_cast<const void*>(&ajx_lane_eval<0, true>),
                             reinterpret_cast<const void*>(&ajx_lane_eval<0, false>),
                             reinterpret_cast<const void*>(&ajx_lane_eval<1, true>),
                             reinterpret_cast<const void*>(&ajx_lane_eval<2, true>),
                             reinterpret_cast<const void*>(&ajx_lane_eval<3, true>),
                             reinterpret_cast<const void*>(&ajx_lane_eval<4, true>)};
-        for (const void* k : ks)
-            if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
-                return e;
-        attr_set[dev] = true;
-    }
+        for (const void* k : ks) {
+            const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (r != hipSuccess) return r;
+        }
+        return hipSuccess;
+    });
+    if (e != hipSuccess) return e;
     const uint32_t grid = (n + kLaneBlock - 1) / kLaneBlock;
 #define AJX_LANE_LAUNCH(M, S)                                                                                 \
     hipLaunchKernelGGL((ajx_lane_eval<M, S>), dim3(grid), dim3(kLaneBlock), lds, stream, d_sets, d_set_of_req,    \
@@ -704,15 +721,17 @@ hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_
         const uint32_t lds = ring_off + (fblock / 64) * kWinRingBytesPerWave;
         hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
-        static bool attr_set = false;
-        if (!attr_set) {
+        static std::atomic<uint64_t> attr_done{0};
+        e = attr_once(attr_done, [] {
             const void* ks[] = {reinterpret_cast<const void*>(&ajx_scan_fast<0, true>),
                                 reinterpret_cast<const void*>(&ajx_scan_fast<0, false>)};
-            for (const void* k : ks)
-                if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
-                    return e;
-            attr_set = true;
-        }
+            for (const void* k : ks) {
+                const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                if (r != hipSuccess) return r;
+            }
+            return hipSuccess;
+        });
+        if (e != hipSuccess) return e;
         if (shared)
             hipLaunchKernelGGL((ajx_scan_fast<0, true>), dim3(fgrid), dim3(fblock), lds, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, ring_off,
@@ -768,25 +787,25 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     const uint32_t lds = ring_off + (block / 64) * kWinRingBytesPerWave;
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    static bool fast_attr_set = false;
-    if (!fast_attr_set) {
+    static std::atomic<uint64_t> attr_done{0};
+    e = attr_once(attr_done, [] {
         const void* ks[] = {reinterpret_cast<const void*>(&ajx_scan_fast<0, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<0, false>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<1, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<2, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fused<true>),
                             reinterpret_cast<const void*>(&ajx_scan_fused<false>)};
-        for (const void* k : ks)
-            if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
-                return e;
+        for (const void* k : ks) {
+            const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (r != hipSuccess) return r;
+        }
         // (the tenant kernel also holds static LDS for __syncthreads_and: ask only for what
         // its launch uses, blob + four window rings)
-        if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ajx_scan_fused_tenant),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     kMaxTenantStageBytes + 4 * kWinRingBytesPerWave)) != hipSuccess)
-            return e;
-        fast_attr_set = true;
-    }
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&ajx_scan_fused_tenant),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   kMaxTenantStageBytes + 4 * kWinRingBytesPerWave);
+    });
+    if (e != hipSuccess) return e;
     if (mode == 1 || mode == 2) {  // profiling ablations of stage A (uniform ruleset only)
         if (!shared) return hipErrorInvalidValue;
         if (mode == 1)

@@ -50,7 +50,8 @@ EXPORTS = [
     "authjx_eval_batch_device", "authjx_eval_batch", "authjx_last_kernel_ms", "authjx_set_exact_scan",
     "authjx_last_exact_count", "authjx_select_batch_device", "authjx_select_batch", "authjx_compile_forest",
     "authjx_select_from_eval_device",
-    "authjx_ruleset_trees",
+    "authjx_ruleset_trees", "authjx_batcher_create", "authjx_batcher_destroy", "authjx_batcher_eval",
+    "authjx_batcher_stats",
 ]
 
 
@@ -118,13 +119,22 @@ def load_library(path: str = LIB_PATH):
         L.authjx_set_exact_scan.restype = C.c_int
         L.authjx_last_exact_count.argtypes = [C.c_void_p]
         L.authjx_last_exact_count.restype = C.c_int64
+        L.authjx_batcher_create.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p)]
+        L.authjx_batcher_create.restype = C.c_int
+        L.authjx_batcher_destroy.argtypes = [C.c_void_p]
+        L.authjx_batcher_destroy.restype = None
+        L.authjx_batcher_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_char_p, C.c_size_t, C.c_uint64,
+                                          C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
+        L.authjx_batcher_eval.restype = C.c_int
+        L.authjx_batcher_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 4
+        L.authjx_batcher_stats.restype = C.c_int
         _lib = L
         return L
 
 
 def _check(rc: int, what: str):
     if rc != 0:
-        names = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ELIMIT"}
+        names = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ELIMIT", -5: "ETIMEDOUT", -6: "ECLOSED"}
         raise AuthjxError(f"{what} failed: {names.get(rc, rc)}")
 
 
@@ -391,3 +401,47 @@ def expression_for(expr) -> CompiledExpression:
         c = CompiledExpression(expr)
         expr._compiled = c
     return c
+
+
+class BatchTimeout(AuthjxError):
+    """The request's deadline passed before its batch was evaluated (AUTHJX_ETIMEDOUT)."""
+
+
+class Batcher:
+    """The micro-batcher (authjx_batcher_*): many threads call eval() with one request
+    each; the native worker forms batches (size / window flush, deadlines, AuthConfig
+    buckets) and evaluates each with one launch on its own stream. ctypes releases the
+    GIL around the blocking call, so Python threads wait concurrently."""
+
+    def __init__(self, ctx: "Context", max_batch: int = 4096, window_us: int = 200, queue_cap: int = 0):
+        L = load_library()
+        h = C.c_void_p()
+        _check(L.authjx_batcher_create(ctx._h, max_batch, window_us, queue_cap, C.byref(h)), "authjx_batcher_create")
+        self.ctx = ctx
+        self._h = h
+
+    def eval(self, ruleset: "Ruleset", doc, timeout_s: float = 0.0):
+        """(tri-states, error indices) of `ruleset`'s trees on one document."""
+        d = _b(doc)
+        nt = max(1, len(ruleset.offsets))
+        tri = (C.c_uint8 * nt)()
+        err = (C.c_int32 * nt)()
+        rc = load_library().authjx_batcher_eval(self._h, ruleset._h, d, len(d), int(timeout_s * 1e6), tri, err)
+        if rc == -5:
+            raise BatchTimeout("authjx_batcher_eval: deadline passed")
+        _check(rc, "authjx_batcher_eval")
+        return list(tri), list(err)
+
+    def stats(self) -> Dict[str, int]:
+        v = [C.c_uint64() for _ in range(4)]
+        _check(load_library().authjx_batcher_stats(self._h, *[C.byref(x) for x in v]), "authjx_batcher_stats")
+        return dict(zip(("batches", "requests", "expired", "max_batch_seen"), (x.value for x in v)))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().authjx_batcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+

@@ -3,10 +3,20 @@
  * pattern-matching authorization hot path.
  *
  * Plain C types only (pointers, sizes, integers); no torch / HIP types in signatures
- * (`stream` is an opaque hipStream_t passed as void*). All functions are reentrant;
- * compiled rulesets are immutable after authjx_compile and may be shared by any number
- * of threads (the reference shares expression trees across goroutines:
- * pkg/service/auth.go:300 copies AuthConfig by value, sharing its trees).
+ * (`stream` is an opaque hipStream_t passed as void*).
+ *
+ * Concurrency: every function may be called from any thread. Compiled rulesets are
+ * immutable after authjx_compile and may be shared by any number of threads and
+ * contexts of their device (the reference shares expression trees across goroutines:
+ * pkg/service/auth.go:300 copies AuthConfig by value, sharing its trees). A context
+ * keeps one workspace (set table, capture rows, exact-scan list, request order) per
+ * stream it is called with: batches on different streams of one context run
+ * concurrently without sharing scratch; calls on one stream are serialised (their
+ * kernels are ordered by the stream). authjx_free waits for the last batch of every
+ * stream that used the ruleset, nothing else. The host-buffer entry points
+ * (authjx_eval_batch, authjx_select_batch) use the context's own stream, one call at a
+ * time. For many concurrent callers with one request each, use the micro-batcher
+ * (authjx_batcher_*), which forms the batches.
  *
  * Interface each entry point replaces (reference = modassarrana89/authorino):
  *   authjx_compile          controllers/auth_config_controller.go:805-852
@@ -55,6 +65,8 @@ extern "C" {
 #define AUTHJX_ENOMEM (-2)
 #define AUTHJX_EDEVICE (-3)
 #define AUTHJX_ELIMIT (-4)
+#define AUTHJX_ETIMEDOUT (-5) /* micro-batcher: the deadline passed before evaluation */
+#define AUTHJX_ECLOSED (-6)   /* micro-batcher: destroyed while the request waited for room */
 
 /* jsonexp.Operator (pkg/jsonexp/expressions.go:12-19) */
 #define AUTHJX_OP_UNKNOWN 0
@@ -219,9 +231,33 @@ int authjx_set_exact_scan(authjx_ctx* ctx, int force);
  * (documents it could not prove gjson-equivalent, e.g. not valid JSON). Synchronises. */
 int64_t authjx_last_exact_count(authjx_ctx* ctx);
 
-/* Kernel-only timing of the last authjx_eval_batch_device on the context stream,
- * measured with HIP events around the dominant kernel (ms). */
+/* Kernel-only timing of the last device call on the context (its stream's events
+ * around the launches, ms). */
 float authjx_last_kernel_ms(authjx_ctx* ctx);
+
+/* ---- micro-batcher --------------------------------------------------------------
+ * Replaces the per-request evaluation made from each request's own goroutine
+ * (pkg/service/auth_pipeline.go:150-164 evaluator goroutines; main.go:69,451 up to 10k
+ * concurrent streams): callers submit one request each and block; a worker thread
+ * flushes a batch when max_batch requests are queued or the oldest has waited
+ * window_us, drops requests whose deadline passed (AUTHJX_ETIMEDOUT, not evaluated),
+ * orders the rest by ruleset (AuthConfig buckets) and evaluates them with one launch on
+ * the batcher's own stream (rulesets of one batch share n_trees; others wait for the
+ * next batch). The queue holds at most queue_cap requests (0: 4 * max_batch); a caller
+ * waits for room up to its deadline. */
+typedef struct authjx_batcher authjx_batcher;
+int authjx_batcher_create(authjx_ctx* ctx, uint32_t max_batch, uint32_t window_us, uint32_t queue_cap,
+                          authjx_batcher** out);
+/* Evaluates what is queued, then stops the worker (callers still waiting for room get
+ * AUTHJX_ECLOSED). */
+void authjx_batcher_destroy(authjx_batcher* b);
+/* Blocking: Expression.Matches of `rs` on one document (copied at batch time; the
+ * buffer must stay valid until return). timeout_us: 0 = no deadline. out_tristate /
+ * out_err_idx (may be NULL): n_trees entries, as authjx_eval_batch writes them. */
+int authjx_batcher_eval(authjx_batcher* b, const authjx_ruleset* rs, const uint8_t* doc, size_t len,
+                        uint64_t timeout_us, uint8_t* out_tristate, int32_t* out_err_idx);
+int authjx_batcher_stats(authjx_batcher* b, uint64_t* batches, uint64_t* requests, uint64_t* expired,
+                         uint64_t* max_batch_seen);
 
 #ifdef __cplusplus
 }

@@ -480,3 +480,62 @@ def test_hard_numbers_on_device(ctx):
     assert (tri == 3).sum() == 0
     assert np.array_equal(tri, otri) and np.array_equal(err, oerr) and np.array_equal(bm, obm)
     assert len(set(tri.tolist())) > 1
+
+
+def test_micro_batcher_concurrent_producers():
+    """8 producer threads x 10^4 requests through three micro-batchers: two on one
+    context (two streams, so two workspaces of that context run concurrently) and one on
+    a second context; mixed AuthConfigs (c4's rulesets): every result equals the oracle;
+    the batchers formed multi-request batches."""
+    import threading
+
+    from authorino_amd import runtime
+    from authorino_amd import workloads as W
+
+    w = W.make("c4", n=4000, seed=41)
+    ctxs = [runtime.Context(0), runtime.Context(0)]
+    used = [int(x) for x in np.unique(w.set_of_req)]
+    sets = [{k: c.compile_expression(w.exprs[k]) for k in used} for c in ctxs]
+    osets = [O.Ruleset(*flat(w.exprs[k])) for k in used]
+    remap = np.zeros(int(w.set_of_req.max()) + 1, dtype=np.uint32)
+    remap[used] = np.arange(len(used), dtype=np.uint32)
+    otri, oerr, _ = O.eval_batch(osets, w.arena, w.offs, w.lens, set_of_req=remap[w.set_of_req], nthreads=8)
+    batchers = [runtime.Batcher(ctxs[k], max_batch=2048, window_us=300) for k in (0, 0, 1)]
+    bad = []
+
+    def producer(t):
+        b = batchers[t % 3]
+        cs = sets[0 if t % 3 < 2 else 1]
+        rng = np.random.default_rng(1000 + t)
+        for _ in range(10000):
+            i = int(rng.integers(0, w.n))
+            tri, err = b.eval(cs[int(w.set_of_req[i])], w.doc(i))
+            if tri[0] != otri[i] or err[0] != oerr[i]:
+                bad.append((t, i, tri, err, int(otri[i]), int(oerr[i])))
+
+    ts = [threading.Thread(target=producer, args=(t,)) for t in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    stats = [b.stats() for b in batchers]
+    for b in batchers:
+        b.close()
+    assert not bad, bad[:5]
+    assert sum(s["requests"] for s in stats) == 80000
+    assert all(s["max_batch_seen"] > 1 for s in stats)
+
+
+def test_pipeline_sets_aside_undecided_requests():
+    """A request whose selected value is a hex number literal (never valid JSON; gjson
+    still reads it as a number) is left undecided by the device: the pipeline marks that
+    request only (AuthResult.undecided) and decides the others of the batch."""
+    from authorino_amd import jsonexp, pipeline
+
+    rules = jsonexp.Pattern("a", jsonexp.Operator.EqualOperator, "0")
+    cfg = pipeline.AuthConfig(authorization=[pipeline.AuthorizationConfig("r", rules=rules)])
+    p = pipeline.AuthPipelineBatch(cfg)
+    res = p.evaluate([b'{"a":0x10}', b'{"a":0}', b'{"a":1}'])
+    assert res[0].undecided and res[0].code == pipeline.CODE_UNKNOWN
+    assert not res[1].undecided and res[1].code == pipeline.CODE_OK
+    assert not res[2].undecided and res[2].code == pipeline.CODE_PERMISSION_DENIED
