@@ -1,15 +1,15 @@
 """Host-side AuthConfig index: per-request AuthConfig selection for multi-tenant batches
 (SURVEY.md §8 a15, config C4).
 
-Restates pkg/index/index.go (the `Index` interface :16-27 and its radix tree :41-260)
+Restates pkg/index/index.go (the `Index` interface :16-27 and its radix tree :37-243)
 and the `:port` retry of pkg/service/auth.go:270-289. Selection stays on the host, as in
 the reference: the micro-batcher resolves each request's host to an AuthConfig id, and
 the device batch carries that id as `set_of_req` (include/authjx.h).
 
 Keys are hostnames. Each '.' starts a new tree level, read from the TLD down
-(`revertKey`, index.go:252-259). A `*` label matches any host below the longest common
+(`revertKey`, index.go:236-243). A `*` label matches any host below the longest common
 path between the searched key and the tree; the search climbs from that node to the
-root, taking the first `*` child that holds an entry (`treeNode.get`, index.go:155-177).
+root, taking the first `*` child that holds an entry (`treeNode.get`, index.go:153-174).
 """
 from __future__ import annotations
 
@@ -17,12 +17,12 @@ from typing import Dict, Iterable, List, Optional, Tuple
 
 import numpy as np
 
-KEY_LABELS_SEPARATOR = "."  # index.go:12
-ROOT_KEY_LABEL = ""          # index.go:13
+KEY_LABELS_SEPARATOR = "."  # index.go:11
+ROOT_KEY_LABEL = ""          # index.go:12
 
 
 class AlreadyExistsError(Exception):
-    """the error `Set` returns for a taken key without override (index.go:183-185)"""
+    """the error `Set` returns for a taken key without override (index.go:180-182)"""
 
 
 class IndexEntry:
@@ -35,7 +35,7 @@ class IndexEntry:
 
 
 class _TreeNode:
-    """index.go:139-152"""
+    """index.go:138-151"""
     __slots__ = ("label", "entry", "parent", "children")
 
     def __init__(self, label: str, parent: Optional["_TreeNode"]):
@@ -45,11 +45,11 @@ class _TreeNode:
         self.children: Dict[str, _TreeNode] = {}
 
     def longest_common_label(self, key: str) -> Tuple["_TreeNode", str]:
-        """index.go:214-235, iteratively: the deepest node on the key's path, and the
+        """index.go:205-223, iteratively: the deepest node on the key's path, and the
         labels of the key below it ("" when the key ends at that node)."""
         labels = key.split(KEY_LABELS_SEPARATOR)
         if self.label != labels[0]:
-            raise RuntimeError("cannot traverse index tree")  # index.go:222-226 (a panic there)
+            raise RuntimeError("cannot traverse index tree")  # index.go:208-213 (a panic there)
         node, i = self, 0
         while i + 1 < len(labels):
             child = node.children.get(labels[i + 1])
@@ -59,7 +59,7 @@ class _TreeNode:
         return node, KEY_LABELS_SEPARATOR.join(labels[i + 1:])
 
     def get(self, key: str) -> Optional[IndexEntry]:
-        """index.go:155-177"""
+        """index.go:153-174"""
         node, tail = self.longest_common_label(key)
         if tail == "" and node.entry is not None:  # the longest common node matches the key
             return node.entry
@@ -74,7 +74,7 @@ class _TreeNode:
         return None
 
     def set(self, key: str, entry: IndexEntry, override: bool) -> Optional[Exception]:
-        """index.go:179-212"""
+        """index.go:176-203"""
         target, tail = self.longest_common_label(key)
         if tail == "":
             if not override:
@@ -92,7 +92,7 @@ class _TreeNode:
         return None
 
     def list(self) -> List[IndexEntry]:
-        """index.go:237-246"""
+        """index.go:225-234"""
         out, stack = [], [self]
         while stack:
             n = stack.pop()
@@ -103,13 +103,13 @@ class _TreeNode:
 
 
 def revert_key(key: str) -> str:
-    """index.go:252-259: "talker-api.nip.io" -> ".io.nip.talker-api" (root label first)"""
+    """index.go:236-243: "talker-api.nip.io" -> ".io.nip.talker-api" (root label first)"""
     labels = key.split(KEY_LABELS_SEPARATOR) + [ROOT_KEY_LABEL]
     return KEY_LABELS_SEPARATOR.join(reversed(labels))
 
 
 class Index:
-    """`index.NewIndex()` (index.go:28-30): the AuthConfig tree (authConfigTree, :41-137).
+    """`index.NewIndex()` (index.go:28-30): the AuthConfig tree (authConfigTree, :37-136).
     Errors are returned, as the Go methods do, rather than raised."""
 
     def __init__(self):

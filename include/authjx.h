@@ -157,7 +157,10 @@ size_t authjx_pattern_error(const authjx_ruleset* rs, uint32_t i, char* buf, siz
 /* Evaluate a batch whose documents are already in device memory (HBM).
  *   sets[n_sets]      rulesets; request r uses sets[set_of_req ? set_of_req[r] : 0]
  *   d_set_of_req      device u32[n] (entries < n_sets) or NULL; ignored when n_sets == 1
- *   d_arena           device bytes; document r = d_arena[d_offs[r] .. + d_lens[r])
+ *   d_arena           device bytes; document r = d_arena[d_offs[r] .. + d_lens[r]). The
+ *                     kernels read whole aligned 16-byte blocks: every block holding a
+ *                     document byte must be readable (device allocations are; an arena
+ *                     carved from a larger buffer needs 15 readable bytes after its end)
  *   d_out_tristate    device u8[n * n_trees]  (AUTHJX_F/T/E/UNDECIDED; n_trees = 1 unless
  *                     the rulesets come from authjx_compile_forest)
  *   d_out_err_idx     device i32[n * n_trees] pattern whose error decided an E, else -1

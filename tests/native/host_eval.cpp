@@ -5,6 +5,7 @@
 #define AJX_HD inline
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../authorino_amd/csrc/ajx_compiler.h"
 #include "../../authorino_amd/csrc/ajx_fast.h"
@@ -32,7 +33,11 @@ void* ht_compile(const authjx_tree* tree, int32_t* status, char* err, size_t cap
 void ht_free(void* h) { delete (HtRuleset*)h; }
 
 // evaluate one document; res[p] receives each pattern's tri-state
-int ht_eval(void* h, const uint8_t* doc, uint32_t len, uint8_t* res, int32_t* err) {
+int ht_eval(void* h, const uint8_t* doc_in, uint32_t len, uint8_t* res, int32_t* err) {
+    // (the device reads whole aligned blocks around a document: give the copy that slack)
+    std::vector<uint8_t> buf(len + 32, 0);
+    uint8_t* doc = buf.data() + 16;
+    if (len) std::memcpy(doc, doc_in, len);
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
     const RulesetHdr* hd = (const RulesetHdr*)blob;
     const Selector* sels = (const Selector*)(blob + hd->off_selectors);
@@ -52,7 +57,10 @@ int ht_eval(void* h, const uint8_t* doc, uint32_t len, uint8_t* res, int32_t* er
 }
 
 // value resolution only: type + raw span
-int ht_get(const char* path, uint32_t plen, const uint8_t* doc, uint32_t len, uint32_t* start, uint32_t* end) {
+int ht_get(const char* path, uint32_t plen, const uint8_t* doc_in, uint32_t len, uint32_t* start, uint32_t* end) {
+    std::vector<uint8_t> buf(len + 32, 0);
+    uint8_t* doc = buf.data() + 16;
+    if (len) std::memcpy(doc, doc_in, len);
     std::vector<PathComponent> pc;
     if (!split_selector(std::string(path, plen), &pc)) return -1;
     std::string lits;
@@ -69,7 +77,10 @@ int ht_get(const char* path, uint32_t plen, const uint8_t* doc, uint32_t len, ui
 }
 
 // Result.String() of the value at path; returns length or -1 undecided / -2 unsupported
-int ht_string(const char* path, uint32_t plen, const uint8_t* doc, uint32_t len, uint8_t* out, uint32_t cap) {
+int ht_string(const char* path, uint32_t plen, const uint8_t* doc_in, uint32_t len, uint8_t* out, uint32_t cap) {
+    std::vector<uint8_t> buf(len + 32, 0);
+    uint8_t* doc = buf.data() + 16;
+    if (len) std::memcpy(doc, doc_in, len);
     std::vector<PathComponent> pc;
     if (!split_selector(std::string(path, plen), &pc)) return -2;
     std::string lits;
