@@ -48,7 +48,7 @@ def parse():
                     help="CPU/gloo test of the distributed driver: no GPU, a stand-in step")
     ap.add_argument("--kernel-mode", type=int, default=0,
                     help="0 the single-pass kernel (default), 20 the lane kernel; others: profiling ablations")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "pmc_traffic.json"))
     return ap.parse_args()
 
 
@@ -328,8 +328,9 @@ def main():
     traffic = None
     try:
         with open(args.pmc_json) as f:
-            pmc = json.load(f)
-        if pmc.get("workload") == args.workload and pmc.get("n") == w.n:
+            pmc = json.load(f).get(args.workload, {})
+        # (measured by scripts/pmc_traffic.py on the same workload, size and kernel)
+        if pmc.get("n") == w.n and args.kernel_mode in (0, 20) and (args.kernel_mode == 20) == ("lane" in pmc.get("kernel", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass

@@ -1,7 +1,8 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py into HBM bytes per
-launch of the dominant kernel (written to profiles/pmc_traffic.json, read by bench.py).
+launch of the dominant kernel, merged per workload into pmc_traffic.json at the repo root
+(read by bench.py for roofline.traffic; a copy goes to profiles/<round>/).
 
-  python scripts/pmc_traffic.py <fetch_dir> <write_dir> <workload> <n> [out.json]
+  python scripts/pmc_traffic.py <fetch_dir> <write_dir> <workload> <n> [out.json] [kernel]
 
 FETCH_SIZE / WRITE_SIZE are reported in KiB. MI355X_MICROARCH.md (HBM/rocprofv3 section):
 FETCH_SIZE counts exactly half the bytes of a wide coalesced streaming read on gfx950;
@@ -28,7 +29,7 @@ def per_launch(d, counter, kernel_sub):
 
 def main():
     fetch_dir, write_dir, workload, n = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
-    out = sys.argv[5] if len(sys.argv) > 5 else "profiles/pmc_traffic.json"
+    out = sys.argv[5] if len(sys.argv) > 5 else "pmc_traffic.json"
     kernel = sys.argv[6] if len(sys.argv) > 6 else "ajx_scan_fused"
     fb, nf = per_launch(fetch_dir, "FETCH_SIZE", kernel)
     wb, nw = per_launch(write_dir, "WRITE_SIZE", kernel)
@@ -43,8 +44,16 @@ def main():
         "note": "FETCH_SIZE+WRITE_SIZE (KiB*1024), median over launches, raw (not doubled): per-lane 16-B "
                 "loads are outside the guide's calibrated access shapes",
     }
+    try:
+        with open(out) as f:
+            allw = json.load(f)
+        if "workload" in allw:  # (an older single-workload file)
+            allw = {allw["workload"]: allw}
+    except (OSError, ValueError):
+        allw = {}
+    allw[workload] = res
     with open(out, "w") as f:
-        json.dump(res, f, indent=1)
+        json.dump(allw, f, indent=1)
     print(json.dumps(res))
 
 
