@@ -366,6 +366,9 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     for (uint32_t i = 0; i < n_sets && fast_tables; i++)
         fast_tables = (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagFastOk) != 0;
     const bool lane = fast_tables && ablate >= 20;
+    bool mods = false;  // modifier chains: the exact scan's instance with text buffers
+    for (uint32_t i = 0; i < n_sets; i++)
+        mods = mods || reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->n_modifiers != 0;
     // capture rows kept for authjx_select_from_eval_device: one ruleset, a full kernel
     const bool full = ablate == 0 || ablate == 20;
     const bool keep_rows = !force_scan && n_sets == 1 && full;
@@ -376,7 +379,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     for (uint32_t i = 0; i < n_sets; i++) max_blob = std::max(max_blob, sets[i]->c.blob.size());
     if (force_scan) {
         HIP_OK(ajx::launch_eval_scan(w->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
-                                     d_out_err_idx, d_out_bitmap, bitmap_stride_words, s));
+                                     d_out_err_idx, d_out_bitmap, bitmap_stride_words, s, mods));
     } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
         // caller's bucketing by AuthConfig), a full kernel, batches worth sorting
@@ -390,7 +393,8 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
                 n_sets == 1 && max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u;
             HIP_OK(ajx::launch_eval_lane(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                          d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
-                                         w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s, ablate - 20, perm));
+                                         w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s, ablate - 20, perm,
+                                         mods));
         } else {
             // uniform batch: the blob staged once per workgroup; multi-tenant batch: the
             // largest blob, for workgroups whose requests share one ruleset
@@ -401,7 +405,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
             HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                          d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
                                          w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
-                                         ablate < 20 ? ablate : 0, perm));
+                                         ablate < 20 ? ablate : 0, perm, mods));
         }
     }
     return batch_done(w, sets, n_sets);

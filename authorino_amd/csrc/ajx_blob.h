@@ -51,6 +51,22 @@ struct Component {
 struct Selector {
     uint32_t comp_begin;
     uint32_t comp_count;
+    uint32_t mod_begin;  // gjson modifiers applied to the path's value (Modifier records)
+    uint32_t mod_count;
+};
+
+// The reference's custom gjson modifiers (pkg/json/json.go:161-264, registered at
+// :258-264), applied in order to the raw JSON of the selected value (a path such as
+// `auth.identity.email.@extract:{"sep":"@","pos":1}|@case:upper`). Evaluated by the
+// exact scan only (ajx_modifiers.h).
+enum : uint8_t { M_EXTRACT = 1, M_REPLACE = 2, M_CASE = 3, M_BASE64 = 4, M_STRIP = 5 };
+struct Modifier {
+    uint8_t kind;
+    uint8_t variant;  // CASE 1 upper / 2 lower; BASE64 1 encode / 2 decode; 0: returns its input
+    uint16_t pad;
+    uint32_t a_off, a_len;  // EXTRACT: sep; REPLACE: old (literal pool)
+    uint32_t b_off, b_len;  // REPLACE: new
+    uint32_t pos;           // EXTRACT: part index
 };
 
 struct Pattern {
@@ -167,7 +183,9 @@ struct RulesetHdr {
     uint32_t key_slots_log2;    // KeySlot table of 1 << key_slots_log2 entries
     uint32_t off_key_slots;
     uint32_t pad1[3];
-    uint32_t pad2[8];
+    uint32_t off_modifiers;     // Modifier[n_modifiers]
+    uint32_t n_modifiers;
+    uint32_t pad2[6];
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
     uint64_t unsupported[2];    // pattern p can not be decided on the device

@@ -1,6 +1,9 @@
 // ajx_compiler.cpp — jsonexp tree -> ruleset blob (see ajx_blob.h for the layout).
 #include "ajx_compiler.h"
 
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -87,6 +90,254 @@ bool split_selector(const std::string& p, std::vector<PathComponent>* out) {
 }
 
 namespace {
+
+// ---- gjson modifier chains (pkg/json/json.go:161-264) ---------------------------------
+struct ModSpec {
+    uint8_t kind = 0, variant = 0;
+    std::string a, b;
+    uint32_t pos = 0;
+};
+
+// gjson's squash of a JSON argument at s[i] ('{' '[' '"'): its end (exclusive), or npos
+size_t squash_arg(const std::string& s, size_t i) {
+    if (s[i] == '"') {
+        for (size_t k = i + 1; k < s.size(); k++) {
+            if (s[k] == '\\') { k++; continue; }
+            if (s[k] == '"') return k + 1;
+        }
+        return std::string::npos;
+    }
+    int depth = 0;
+    for (size_t k = i; k < s.size(); k++) {
+        const char c = s[k];
+        if (c == '"') {
+            for (k++; k < s.size(); k++) {
+                if (s[k] == '\\') { k++; continue; }
+                if (s[k] == '"') break;
+            }
+            if (k >= s.size()) return std::string::npos;
+            continue;
+        }
+        if (c == '{' || c == '[' || c == '(') depth++;
+        if (c == '}' || c == ']' || c == ')') {
+            if (--depth == 0) return k + 1;
+        }
+    }
+    return std::string::npos;
+}
+
+void put_utf8(uint32_t r, std::string* o) {
+    if (r > 0x10FFFF || (r >= 0xD800 && r < 0xE000)) r = 0xFFFD;
+    if (r < 0x80) o->push_back((char)r);
+    else if (r < 0x800) { o->push_back((char)(0xC0 | (r >> 6))); o->push_back((char)(0x80 | (r & 0x3F))); }
+    else if (r < 0x10000) {
+        o->push_back((char)(0xE0 | (r >> 12))); o->push_back((char)(0x80 | ((r >> 6) & 0x3F)));
+        o->push_back((char)(0x80 | (r & 0x3F)));
+    } else {
+        o->push_back((char)(0xF0 | (r >> 18))); o->push_back((char)(0x80 | ((r >> 12) & 0x3F)));
+        o->push_back((char)(0x80 | ((r >> 6) & 0x3F))); o->push_back((char)(0x80 | (r & 0x3F)));
+    }
+}
+
+// a JSON string token at s[i] ('"') -> its unescaped text; false if not well formed
+bool json_string_at(const std::string& s, size_t* i, std::string* out) {
+    out->clear();
+    size_t k = *i + 1;
+    auto hex4 = [&](size_t at, uint32_t* v) {
+        if (at + 4 > s.size()) return false;
+        uint32_t x = 0;
+        for (size_t j = 0; j < 4; j++) {
+            const char c = s[at + j];
+            x <<= 4;
+            if (c >= '0' && c <= '9') x |= (uint32_t)(c - '0');
+            else if ((c | 0x20) >= 'a' && (c | 0x20) <= 'f') x |= (uint32_t)((c | 0x20) - 'a' + 10);
+            else return false;
+        }
+        *v = x;
+        return true;
+    };
+    for (; k < s.size(); k++) {
+        const char c = s[k];
+        if (c == '"') { *i = k + 1; return true; }
+        if ((unsigned char)c < 0x20) return false;
+        if (c != '\\') { out->push_back(c); continue; }
+        if (++k >= s.size()) return false;
+        switch (s[k]) {
+            case '"': out->push_back('"'); break;
+            case '\\': out->push_back('\\'); break;
+            case '/': out->push_back('/'); break;
+            case 'b': out->push_back('\b'); break;
+            case 'f': out->push_back('\f'); break;
+            case 'n': out->push_back('\n'); break;
+            case 'r': out->push_back('\r'); break;
+            case 't': out->push_back('\t'); break;
+            case 'u': {
+                uint32_t r;
+                if (!hex4(k + 1, &r)) return false;
+                k += 4;
+                if (r >= 0xD800 && r < 0xDC00 && k + 6 < s.size() + 0 && s[k + 1] == '\\' && s[k + 2] == 'u') {
+                    uint32_t r2;
+                    if (hex4(k + 3, &r2) && r2 >= 0xDC00 && r2 < 0xE000) {
+                        r = (((r - 0xD800) << 10) | (r2 - 0xDC00)) + 0x10000;
+                        k += 6;
+                    }
+                }
+                put_utf8(r, out);
+                break;
+            }
+            default: return false;
+        }
+    }
+    return false;
+}
+
+// the members of a JSON object argument ({"sep":"@","pos":1}): key -> ('s', text) for
+// strings, ('n', raw) for numbers, ('o', raw) otherwise; false if not a plain object
+bool object_members(const std::string& a, std::vector<std::pair<std::string, std::pair<char, std::string>>>* m) {
+    size_t i = 0;
+    auto ws = [&] { while (i < a.size() && (unsigned char)a[i] <= ' ') i++; };
+    ws();
+    if (i >= a.size() || a[i] != '{') return false;
+    i++;
+    ws();
+    if (i < a.size() && a[i] == '}') return true;
+    for (;;) {
+        ws();
+        std::string key, val;
+        if (i >= a.size() || a[i] != '"' || !json_string_at(a, &i, &key)) return false;
+        ws();
+        if (i >= a.size() || a[i] != ':') return false;
+        i++;
+        ws();
+        if (i >= a.size()) return false;
+        char kind;
+        if (a[i] == '"') {
+            if (!json_string_at(a, &i, &val)) return false;
+            kind = 's';
+        } else {
+            const size_t b = i;
+            if (a[i] == '{' || a[i] == '[') {
+                const size_t e = squash_arg(a, i);
+                if (e == std::string::npos) return false;
+                i = e;
+                kind = 'o';
+            } else {
+                while (i < a.size() && a[i] != ',' && a[i] != '}' && (unsigned char)a[i] > ' ') i++;
+                kind = (a[b] == '-' || (a[b] >= '0' && a[b] <= '9')) ? 'n' : 'o';
+            }
+            val = a.substr(b, i - b);
+        }
+        m->push_back({key, {kind, val}});
+        ws();
+        if (i < a.size() && a[i] == ',') { i++; continue; }
+        if (i < a.size() && a[i] == '}') return true;
+        return false;
+    }
+}
+
+// Split `path` into a plain base path and a chain of the reference's modifiers, as
+// gjson.Get runs it: parseObjectPath pipes at '|' or at '.' before '@'
+// (isDotPiperChar); execModifier reads a name up to ':' '|' '.', a JSON argument by
+// squash or a plain one up to the next '|'; the result goes on through '|' or '.'.
+// 0: no modifier; 1: base + mods; -1: a form the device does not evaluate (other
+// modifiers, a path after a modifier, arguments outside the supported ones).
+int split_modifiers(const std::string& path, std::string* base, std::vector<ModSpec>* mods) {
+    mods->clear();
+    size_t cut = std::string::npos;
+    for (size_t i = 0; i + 1 < path.size(); i++) {
+        if (path[i] == '\\') { i++; continue; }
+        if ((path[i] == '.' || path[i] == '|') && path[i + 1] == '@') { cut = i; break; }
+    }
+    if (cut == std::string::npos || cut == 0) return 0;
+    *base = path.substr(0, cut);
+    size_t i = cut + 1;  // at '@'
+    while (i < path.size()) {
+        if (path[i] != '@') return -1;  // a path component after a modifier
+        size_t k = i + 1;
+        while (k < path.size() && path[k] != ':' && path[k] != '|' && path[k] != '.') k++;
+        const std::string name = path.substr(i + 1, k - i - 1);
+        std::string arg;
+        bool has_args = false;
+        size_t next = k;
+        if (k < path.size() && path[k] == ':') {
+            const size_t a = k + 1;
+            has_args = a < path.size();
+            if (has_args && (path[a] == '{' || path[a] == '[' || path[a] == '"')) {
+                const size_t e = squash_arg(path, a);
+                if (e == std::string::npos) return -1;
+                arg = path.substr(a, e - a);
+                next = e;
+            } else {
+                size_t e = path.find('|', a);
+                if (e == std::string::npos) e = path.size();
+                arg = path.substr(a, e - a);
+                next = e;
+            }
+        }
+        ModSpec m;
+        if (name == "extract") {
+            m.kind = M_EXTRACT;
+            m.a = " ";
+            m.pos = 0;
+            std::vector<std::pair<std::string, std::pair<char, std::string>>> mem;
+            if (has_args && !arg.empty() && arg[0] == '{') {
+                if (!object_members(arg, &mem)) return -1;
+                for (auto& kv : mem) {
+                    if (kv.first == "sep") {
+                        if (kv.second.first != 's') return -1;
+                        m.a = kv.second.second;
+                    } else if (kv.first == "pos") {
+                        if (kv.second.first != 'n') return -1;
+                        char* endp = nullptr;
+                        const double v = std::strtod(kv.second.second.c_str(), &endp);
+                        if (!endp || *endp || !(v >= 0) || v > 9007199254740991.0) return -1;
+                        m.pos = (uint32_t)std::min<double>(std::trunc(v), 0xFFFFFFF0u);
+                    }
+                }
+            } else if (has_args && !arg.empty() && arg[0] != '[' && arg[0] != '"') {
+                // a scalar argument: gjson ForEach visits it with an empty key (defaults)
+            } else if (has_args && !arg.empty()) {
+                return -1;
+            }
+            if (m.a.empty()) return -1;  // strings.Split on "" splits into runes
+        } else if (name == "replace") {
+            m.kind = M_REPLACE;
+            if (has_args && !arg.empty()) {
+                std::vector<std::pair<std::string, std::pair<char, std::string>>> mem;
+                if (arg[0] != '{' || !object_members(arg, &mem)) return -1;
+                bool have_old = false;
+                for (auto& kv : mem) {
+                    if (kv.first == "old") {
+                        if (kv.second.first != 's') return -1;
+                        m.a = kv.second.second;
+                        have_old = true;
+                    } else if (kv.first == "new") {
+                        if (kv.second.first != 's') return -1;
+                        m.b = kv.second.second;
+                    }
+                }
+                if (!have_old || m.a.empty()) return -1;  // ReplaceAll with "" inserts between runes
+                m.variant = 1;
+            }
+        } else if (name == "case") {
+            m.kind = M_CASE;
+            m.variant = arg == "upper" ? 1 : arg == "lower" ? 2 : 0;
+        } else if (name == "base64") {
+            m.kind = M_BASE64;
+            m.variant = arg == "encode" ? 1 : arg == "decode" ? 2 : 0;
+        } else if (name == "strip") {
+            m.kind = M_STRIP;
+        } else {
+            return -1;  // gjson's own modifiers (@this, @reverse, @fromstr, ...) are not compiled
+        }
+        mods->push_back(m);
+        if (next >= path.size()) break;
+        if (path[next] != '|' && path[next] != '.') return -1;
+        i = next + 1;
+        if (i >= path.size()) return -1;
+    }
+    return mods->empty() ? -1 : 1;
+}
 
 struct NormNode {
     int kind;  // 0 = AND, 1 = OR, 2 = leaf pattern, 3 = const T, 4 = const F
@@ -237,6 +488,7 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     std::map<std::string, uint32_t> sel_ids;
     std::vector<Selector> sels;
     std::vector<Component> comps;
+    std::vector<Modifier> mods;  // modifier chains of the selectors
     std::vector<Pattern> pats(np);
     std::vector<RegexDfa> dfas;
     std::vector<int> dfa_of(np, -1);
@@ -286,7 +538,10 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         auto it = sel_ids.find(sel);
         if (it == sel_ids.end()) {
             std::vector<PathComponent> pc;
-            if (!split_selector(sel, &pc)) {
+            std::string base = sel;
+            std::vector<ModSpec> mspec;
+            const int mr = split_modifiers(sel, &base, &mspec);
+            if (mr < 0 || !split_selector(base, &pc)) {
                 p.state = P_UNSUPPORTED;
                 out->pattern_status[i] = AUTHJX_PAT_UNSUPPORTED;
                 out->pattern_error[i] = "selector syntax not compiled for the device";
@@ -296,6 +551,22 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             Selector s;
             s.comp_begin = (uint32_t)comps.size();
             s.comp_count = (uint32_t)pc.size();
+            s.mod_begin = (uint32_t)mods.size();
+            s.mod_count = (uint32_t)mspec.size();
+            for (const ModSpec& m : mspec) {
+                Modifier r;
+                std::memset(&r, 0, sizeof r);
+                r.kind = m.kind;
+                r.variant = m.variant;
+                r.a_off = (uint32_t)lits.size();
+                r.a_len = (uint32_t)m.a.size();
+                lits += m.a;
+                r.b_off = (uint32_t)lits.size();
+                r.b_len = (uint32_t)m.b.size();
+                lits += m.b;
+                r.pos = m.pos;
+                mods.push_back(r);
+            }
             for (const PathComponent& c : pc) {
                 Component k;
                 k.lit_off = (uint32_t)lits.size();
@@ -320,7 +591,8 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     std::vector<TNode> trie(1);
     std::vector<std::vector<uint16_t>> sel_pats(sels.size());
     uint64_t null_true[2] = {0, 0}, static_err[2] = {0, 0}, unsup[2] = {0, 0};
-    bool fast_ok = np <= kFastMaxPatterns && sels.size() <= kFastMaxSelectors;
+    // (modifier chains run in the exact scan only: such a ruleset has no single-pass tables)
+    bool fast_ok = np <= kFastMaxPatterns && sels.size() <= kFastMaxSelectors && mods.empty();
     for (size_t s = 0; s < sels.size() && fast_ok; s++) {
         uint32_t cur = 0;
         for (uint32_t k = 0; k < sels[s].comp_count; k++) {
@@ -439,6 +711,9 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             hdr.unsupported[k] = unsup[k];
         }
     }
+    hdr.n_modifiers = (uint32_t)mods.size();
+    hdr.off_modifiers = (uint32_t)b.align16();
+    b.append(mods.data(), mods.size() * sizeof(Modifier));
     hdr.off_selectors = (uint32_t)b.align16();
     b.append(sels.data(), sels.size() * sizeof(Selector));
     hdr.off_components = (uint32_t)b.align16();

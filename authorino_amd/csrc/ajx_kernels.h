@@ -7,7 +7,7 @@ namespace ajx {
 
 hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
                             const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
-                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream);
+                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream, bool mods = false);
 
 // gjson.Get of every pattern's selector: d_out = u32[n][stride][3] {start, len, type | esc << 8}.
 // With d_rows: the single-pass stage A captures all spans in one scan per document (rows of
@@ -34,6 +34,8 @@ constexpr uint32_t kMaxSharedBlobBytes = 48 * 1024;
 // window rings (blob + 4 x 8 KiB rings per group keeps 4 groups = 4 waves/SIMD per CU)
 constexpr uint32_t kMaxTenantStageBytes = 8 * 1024;
 
+// `mods` (every launcher): a ruleset of the batch has modifier chains (RulesetHdr
+// n_modifiers); the exact scan then runs its instance with modifier buffers.
 // single-pass kernel + exact scan of the requests it hands over (d_slow_count is zeroed
 // on the stream first; d_slow_ids needs room for n entries). shared_blob_bytes: the
 // blob size of sets[0] when every request uses it and it fits kMaxSharedBlobBytes,
@@ -44,7 +46,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode = 0, const uint32_t* d_perm = nullptr);
+                            int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false);
 
 // The lane kernel (ajx_lane.h): one work-item per request over 64-byte windows the
 // wavefront stages through LDS with coalesced loads; stage B in the same work-item;
@@ -57,7 +59,7 @@ hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode = 0, const uint32_t* d_perm = nullptr);
+                            int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false);
 
 // Length-bucketed request order for the single-pass kernel: d_perm[n] = request ids,
 // longest 8-byte length class first; d_hist needs 2 * 1024 + 1 u32 of scratch.

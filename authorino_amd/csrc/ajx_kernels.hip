@@ -17,6 +17,7 @@
 
 #include "ajx_fast.h"
 #include "ajx_lane.h"
+#include "ajx_modifiers.h"
 #include "ajx_kernels.h"
 
 namespace ajx {
@@ -39,12 +40,15 @@ static hipError_t attr_once(std::atomic<uint64_t>& done, F set) {
 constexpr int kSelCache = 32;  // resolved selector values kept per request
 constexpr int kPatCache = 64;  // pattern results kept per request for the fold
 
+// MODS: the rulesets of the batch have modifier chains (ajx_modifiers.h; mb: the
+// work-item's three text buffers, the caller's scratch)
+template <bool MODS>
 __device__ __forceinline__ void eval_scan_one(uint32_t r, const uint8_t* const* __restrict__ sets,
                                               const uint32_t* __restrict__ set_of_req,
                                               const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                                               const uint32_t* __restrict__ lens, uint8_t* __restrict__ out_tri,
                                               int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
-                                              uint32_t stride) {
+                                              uint32_t stride, [[maybe_unused]] ModBufs* mb) {
     const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const Selector* sels = reinterpret_cast<const Selector*>(blob + h->off_selectors);
@@ -70,6 +74,15 @@ __device__ __forceinline__ void eval_scan_one(uint32_t r, const uint8_t* const* 
     auto eval = [&](uint32_t p) -> uint8_t {
         const Pattern& pt = pats[p];
         if (pt.state != P_OK) return eval_pattern<true>(blob, pt, doc, ValueRef{0, 0, T_NULL, 0});
+        if constexpr (MODS) {
+            const Selector& sl = sels[pt.selector];
+            if (sl.mod_count) {
+                const uint8_t* rd;
+                ValueRef rv;
+                if (!apply_modifiers(blob, sl, doc, value_of(p), *mb, &rd, &rv)) return V_U;
+                return eval_pattern<true>(blob, pt, rd, rv);
+            }
+        }
         return eval_pattern<true>(blob, pt, doc, value_of(p));
     };
 
@@ -108,6 +121,7 @@ __device__ __forceinline__ void eval_scan_one(uint32_t r, const uint8_t* const* 
     }
 }
 
+template <bool MODS>
 __global__ __launch_bounds__(256) void ajx_eval_scan(const uint8_t* const* __restrict__ sets,
                                                      const uint32_t* __restrict__ set_of_req,
                                                      const uint8_t* __restrict__ arena,
@@ -117,10 +131,16 @@ __global__ __launch_bounds__(256) void ajx_eval_scan(const uint8_t* const* __res
                                                      uint64_t* __restrict__ out_bm, uint32_t stride) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
-    eval_scan_one(r, sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride);
+    if constexpr (MODS) {
+        ModBufs mb;
+        eval_scan_one<true>(r, sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride, &mb);
+    } else {
+        eval_scan_one<false>(r, sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride, nullptr);
+    }
 }
 
 // the slow list: grid-stride over the ids the fast kernel appended
+template <bool MODS>
 __global__ __launch_bounds__(256) void ajx_eval_scan_list(const uint8_t* const* __restrict__ sets,
                                                           const uint32_t* __restrict__ set_of_req,
                                                           const uint8_t* __restrict__ arena,
@@ -131,8 +151,30 @@ __global__ __launch_bounds__(256) void ajx_eval_scan_list(const uint8_t* const* 
                                                           uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
                                                           uint64_t* __restrict__ out_bm, uint32_t stride) {
     const uint32_t cnt = *slow_count;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x)
-        eval_scan_one(slow_ids[i], sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride);
+    if constexpr (MODS) {
+        ModBufs mb;
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x)
+            eval_scan_one<true>(slow_ids[i], sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride,
+                                &mb);
+    } else {
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x)
+            eval_scan_one<false>(slow_ids[i], sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride,
+                                 nullptr);
+    }
+}
+
+// the exact scan over the slow list; the instance with modifier buffers when the batch's
+// rulesets have modifier chains
+static void launch_slow_list(bool mods, uint32_t sgrid, hipStream_t stream, const uint8_t* const* d_sets,
+                             const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
+                             const uint32_t* d_lens, const uint32_t* d_slow_count, const uint32_t* d_slow_ids,
+                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride) {
+    if (mods)
+        hipLaunchKernelGGL(ajx_eval_scan_list<true>, dim3(sgrid), dim3(256), 0, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
+    else
+        hipLaunchKernelGGL(ajx_eval_scan_list<false>, dim3(sgrid), dim3(256), 0, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
 }
 
 // SHARED kernels: the whole batch uses sets[0], and the ruleset blob (trie, key table,
@@ -503,7 +545,7 @@ hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode, const uint32_t* d_perm) {
+                            int mode, const uint32_t* d_perm, bool mods) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
     const uint32_t blob_region = shared ? (shared_blob_bytes + 15u) & ~15u : 0u;
@@ -547,8 +589,8 @@ hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mode == 1 || mode == 2 || mode == 4) return hipSuccess;
     const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
-    hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(256), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                       d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
+    launch_slow_list(mods, sgrid, stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids,
+                     d_tri, d_err, d_bm, stride);
     return hipGetLastError();
 }
 
@@ -762,12 +804,16 @@ hipError_t launch_select_rows(const uint8_t* const* d_sets, const uint8_t* d_are
 
 hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
                             const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint8_t* d_tri,
-                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream) {
+                            int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream, bool mods) {
     if (n == 0) return hipSuccess;
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
-    hipLaunchKernelGGL(ajx_eval_scan, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                       d_lens, n, d_tri, d_err, d_bm, stride);
+    if (mods)
+        hipLaunchKernelGGL(ajx_eval_scan<true>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, n, d_tri, d_err, d_bm, stride);
+    else
+        hipLaunchKernelGGL(ajx_eval_scan<false>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, n, d_tri, d_err, d_bm, stride);
     return hipGetLastError();
 }
 
@@ -775,7 +821,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode, const uint32_t* d_perm) {
+                            int mode, const uint32_t* d_perm, bool mods) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
     // small blobs: 4-wave groups (measured faster on c2); larger ones share one copy per
@@ -849,8 +895,8 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
-    hipLaunchKernelGGL(ajx_eval_scan_list, dim3(sgrid), dim3(256), 0, stream, d_sets, d_set_of_req, d_arena,
-                       d_offs, d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
+    launch_slow_list(mods, sgrid, stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids,
+                     d_tri, d_err, d_bm, stride);
     return hipGetLastError();
 }
 

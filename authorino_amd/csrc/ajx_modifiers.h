@@ -1,0 +1,388 @@
+// ajx_modifiers.h — the reference's gjson modifiers on the device (exact scan only):
+// pkg/json/json.go:161-264, registered globally at :258-264. A selector such as
+// `auth.identity.email.@extract:{"sep":"@","pos":1}|@case:upper` is its base path (gj_get)
+// followed by a chain of Modifier records (ajx_blob.h); gjson runs each modifier on the
+// previous result's raw JSON text and parses the last output (gjson.Parse) into the
+// Result the pattern compares. The texts are materialised in three work-item buffers.
+//
+//   extract  Parse(json).String() split on sep; part pos wrapped in quotes, "n" past the end
+//   replace  Parse(json).String() with every old -> new, wrapped (no argument: unchanged)
+//   case     strings.ToUpper / ToLower of the raw text (upper / lower; else unchanged)
+//   base64   encode: StdEncoding of Parse(json).String(), wrapped; decode: StdEncoding when
+//            the length is a multiple of 4 and it decodes, else RawStdEncoding's partial
+//            result; quotes escaped, wrapped (else unchanged)
+//   strip    the runes unicode.IsPrint keeps, of the raw text
+// Unicode case mapping and IsPrint beyond ASCII, texts over kModBuf bytes and Parse of a
+// text starting with an uncommon number character ('+' 'i' 'I' 'N', "n" not "null") are
+// left undecided (the request's pattern is AUTHJX_UNDECIDED).
+#pragma once
+#include "ajx_device.h"
+
+namespace ajx {
+
+constexpr uint32_t kModBuf = 2048;
+
+struct ModBufs {
+    uint8_t a[kModBuf], b[kModBuf], t[kModBuf];
+};
+
+struct OutBuf {
+    uint8_t* p;
+    uint32_t n, cap;
+    bool ok;
+    AJX_HD void put(uint32_t c) {
+        if (n < cap) p[n++] = (uint8_t)c;
+        else ok = false;
+    }
+    AJX_HD void put(const uint8_t* s, uint32_t len) {
+        for (uint32_t i = 0; i < len; i++) put(s[i]);
+    }
+};
+
+// gjson tostr on j[i..n) (j[i] == '"'): the end of the contents (*str_end) and whether
+// they need unescape; returns false when no closing quote ends them (the contents then
+// run to the end of the text)
+AJX_HD bool mod_tostr(const uint8_t* j, uint32_t n, uint32_t i, uint32_t* str_end, bool* esc) {
+    for (uint32_t k = i + 1; k < n; k++) {
+        if (j[k] > '\\') continue;
+        if (j[k] == '"') {
+            *str_end = k;
+            *esc = false;
+            return true;
+        }
+        if (j[k] == '\\') {
+            for (; k < n; k++) {
+                if (j[k] > '\\') continue;
+                if (j[k] == '"') {
+                    if (j[k - 1] == '\\') {
+                        uint32_t nb = 0;
+                        for (uint32_t q = k - 2; q > i && q < k; q--) {
+                            if (j[q] != '\\') break;
+                            nb++;
+                        }
+                        if (nb % 2 == 0) continue;
+                    }
+                    *str_end = k;
+                    *esc = true;
+                    return true;
+                }
+            }
+            *str_end = n;
+            *esc = true;
+            return false;
+        }
+    }
+    *str_end = n;
+    *esc = false;
+    return false;
+}
+
+// gjson tonum extent of a number at j[i]
+AJX_HD uint32_t mod_tonum(const uint8_t* j, uint32_t n, uint32_t i) {
+    for (uint32_t k = i + 1; k < n; k++) {
+        if (j[k] <= '-') {
+            if (j[k] <= ' ' || j[k] == ',') return k;
+        } else if (j[k] == ']' || j[k] == '}') {
+            return k;
+        }
+    }
+    return n;
+}
+AJX_HD uint32_t mod_tolit(const uint8_t* j, uint32_t n, uint32_t i) {
+    for (uint32_t k = i + 1; k < n; k++)
+        if (j[k] < 'a' || j[k] > 'z') return k;
+    return n;
+}
+
+// gjson.Parse(j[0..n)) as a value over a text; `spare` receives an unterminated string's
+// contents re-quoted. Returns false when undecided.
+AJX_HD bool mod_parse(const uint8_t* j, uint32_t n, uint8_t* spare, const uint8_t** rdoc, ValueRef* v) {
+    *rdoc = j;
+    v->start = v->end = 0;
+    v->type = T_NULL;
+    v->esc = 0;
+    uint32_t i = 0;
+    while (i < n && j[i] <= ' ') i++;
+    if (i >= n) return true;  // nothing: not found (Null)
+    const uint8_t c = j[i];
+    if (c == '{' || c == '[') {
+        v->start = i;
+        v->end = n;
+        v->type = T_JSON;
+        return true;
+    }
+    if (c == '"') {
+        uint32_t se;
+        bool esc;
+        if (mod_tostr(j, n, i, &se, &esc)) {
+            v->start = i;
+            v->end = se + 1;
+            v->type = T_STRING;
+            v->esc = esc ? 1 : 0;
+            return true;
+        }
+        // unterminated: the contents j[i+1..n), unescaped when a backslash came first
+        OutBuf o{spare, 0, kModBuf, true};
+        o.put('"');
+        if (esc) {
+            StrSrc s;
+            s.init_unesc(j, i + 1, n);
+            for (int ch; (ch = s.next()) >= 0;) o.put((uint32_t)ch);
+        } else {
+            o.put(j + i + 1, n - i - 1);
+        }
+        o.put('"');
+        if (!o.ok) return false;
+        *rdoc = spare;
+        v->start = 0;
+        v->end = o.n;
+        v->type = T_STRING;
+        return true;
+    }
+    if (c == '-' || (c >= '0' && c <= '9')) {
+        v->start = i;
+        v->end = mod_tonum(j, n, i);
+        v->type = T_NUMBER;
+        return true;
+    }
+    if (c == 't' || c == 'f' || (c == 'n' && (i + 1 >= n || j[i + 1] == 'u'))) {
+        v->start = i;
+        v->end = mod_tolit(j, n, i);
+        v->type = c == 't' ? T_TRUE : c == 'f' ? T_FALSE : T_NULL;
+        return true;
+    }
+    return false;  // '+' 'i' 'I' 'N', "n..." as NaN, other bytes: undecided
+}
+
+// gjson.Parse(j).String() into o; false when undecided
+AJX_HD bool mod_result_string(const uint8_t* j, uint32_t n, uint8_t* spare, OutBuf& o) {
+    const uint8_t* d;
+    ValueRef v;
+    if (!mod_parse(j, n, spare, &d, &v)) return false;
+    StrSrc s;
+    if (!string_of<true>(d, v, &s)) return false;
+    for (int ch; (ch = s.next()) >= 0;) o.put((uint32_t)ch);
+    return o.ok;
+}
+
+AJX_HD uint32_t b64_val(uint8_t c) {
+    if (c >= 'A' && c <= 'Z') return c - 'A';
+    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+    if (c >= '0' && c <= '9') return c - '0' + 52;
+    if (c == '+') return 62;
+    if (c == '/') return 63;
+    return 0xFF;
+}
+
+// encoding/base64 Decode (StdEncoding when pad, else RawStdEncoding; not strict): the
+// bytes written before the first error go to o; returns true when the whole input
+// decoded (Go: err == nil)
+AJX_HD bool b64_decode(const uint8_t* s, uint32_t n, bool pad, OutBuf& o) {
+    uint32_t si = 0;
+    for (;;) {
+        uint32_t q[4];
+        uint32_t jn = 0, dlen = 4;
+        bool err = false, end = false;
+        for (uint32_t j = 0; j < 4; j++) {
+            if (si == n) {
+                if (j == 0) return true;  // clean end
+                if (j == 1 || pad) return false;
+                dlen = j;
+                end = true;
+                break;
+            }
+            const uint8_t in = s[si++];
+            const uint32_t v = b64_val(in);
+            if (v != 0xFF) {
+                q[j] = v;
+                jn = j + 1;
+                continue;
+            }
+            if (in == '\n' || in == '\r') {
+                j--;
+                continue;
+            }
+            if (!pad || in != '=') return false;
+            // padding
+            if (j < 2) return false;
+            if (j == 2) {
+                while (si < n && (s[si] == '\n' || s[si] == '\r')) si++;
+                if (si == n || s[si] != '=') return false;
+                si++;
+            }
+            while (si < n && (s[si] == '\n' || s[si] == '\r')) si++;
+            if (si < n) err = true;
+            dlen = j;
+            end = true;
+            break;
+        }
+        (void)jn;
+        for (uint32_t j = dlen; j < 4; j++) q[j] = 0;
+        const uint32_t val = (q[0] << 18) | (q[1] << 12) | (q[2] << 6) | q[3];
+        if (dlen >= 2) o.put((val >> 16) & 0xFF);
+        if (dlen >= 3) o.put((val >> 8) & 0xFF);
+        if (dlen >= 4) o.put(val & 0xFF);
+        if (err) return false;
+        if (end) return true;
+    }
+}
+
+AJX_HD void b64_encode(const uint8_t* s, uint32_t n, OutBuf& o) {
+    const char* al = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+    uint32_t i = 0;
+    for (; i + 3 <= n; i += 3) {
+        const uint32_t v = ((uint32_t)s[i] << 16) | ((uint32_t)s[i + 1] << 8) | s[i + 2];
+        o.put((uint8_t)al[(v >> 18) & 63]);
+        o.put((uint8_t)al[(v >> 12) & 63]);
+        o.put((uint8_t)al[(v >> 6) & 63]);
+        o.put((uint8_t)al[v & 63]);
+    }
+    if (n - i == 1) {
+        const uint32_t v = (uint32_t)s[i] << 16;
+        o.put((uint8_t)al[(v >> 18) & 63]);
+        o.put((uint8_t)al[(v >> 12) & 63]);
+        o.put('=');
+        o.put('=');
+    } else if (n - i == 2) {
+        const uint32_t v = ((uint32_t)s[i] << 16) | ((uint32_t)s[i + 1] << 8);
+        o.put((uint8_t)al[(v >> 18) & 63]);
+        o.put((uint8_t)al[(v >> 12) & 63]);
+        o.put((uint8_t)al[(v >> 6) & 63]);
+        o.put('=');
+    }
+}
+
+// '"' + escapeQuotes(s) + '"' (json.go escapeQuotes: '"' -> '\"', nothing else)
+AJX_HD void wrap_escaped(const uint8_t* s, uint32_t n, OutBuf& o) {
+    o.put('"');
+    for (uint32_t i = 0; i < n; i++) {
+        if (s[i] == '"') o.put('\\');
+        o.put(s[i]);
+    }
+    o.put('"');
+}
+
+// Run the selector's modifier chain on the value v of document doc: the final gjson
+// Result as (*rdoc, *rv). Returns false when undecided. A value that does not exist stays
+// Null (gjson pipes into the modifiers only from a found value).
+AJX_HD bool apply_modifiers(const uint8_t* blob, const Selector& sel, const uint8_t* doc, const ValueRef& v,
+                            ModBufs& mb, const uint8_t** rdoc, ValueRef* rv) {
+    if (v.end <= v.start) {
+        *rdoc = doc;
+        *rv = v;
+        return true;
+    }
+    const RulesetHdr* h = (const RulesetHdr*)blob;
+    const Modifier* mods = (const Modifier*)(blob + h->off_modifiers) + sel.mod_begin;
+    const uint8_t* lits = blob + h->off_literals;
+    const uint8_t* in = doc + v.start;
+    uint32_t in_n = v.end - v.start;
+    uint8_t* bufs[2] = {mb.a, mb.b};
+    for (uint32_t k = 0; k < sel.mod_count; k++) {
+        const Modifier m = mods[k];
+        uint8_t* outp = bufs[k & 1];
+        OutBuf o{outp, 0, kModBuf, true};
+        OutBuf t{mb.t, 0, kModBuf, true};
+        switch (m.kind) {
+            case M_EXTRACT: {
+                if (!mod_result_string(in, in_n, outp, t)) return false;
+                const uint8_t* sep = lits + m.a_off;
+                const uint32_t sl = m.a_len;
+                uint32_t part = 0, ps = 0, i = 0;
+                bool done = false;
+                while (!done) {
+                    // the next separator at or after i (or the end)
+                    uint32_t e = i;
+                    while (e + sl <= t.n && !bytes_equal(mb.t + e, sep, sl)) e++;
+                    const bool last = e + sl > t.n;
+                    if (last) e = t.n;
+                    if (part == m.pos) {
+                        o.put('"');
+                        o.put(mb.t + ps, e - ps);
+                        o.put('"');
+                        done = true;
+                        break;
+                    }
+                    if (last) break;
+                    part++;
+                    i = e + sl;
+                    ps = i;
+                }
+                if (!done) o.put('n');
+                break;
+            }
+            case M_REPLACE: {
+                if (m.variant == 0) {
+                    o.put(in, in_n);
+                    break;
+                }
+                if (!mod_result_string(in, in_n, outp, t)) return false;
+                const uint8_t* old = lits + m.a_off;
+                o.put('"');
+                uint32_t i = 0;
+                while (i < t.n) {
+                    if (i + m.a_len <= t.n && bytes_equal(mb.t + i, old, m.a_len)) {
+                        o.put(lits + m.b_off, m.b_len);
+                        i += m.a_len;
+                    } else {
+                        o.put(mb.t[i++]);
+                    }
+                }
+                o.put('"');
+                break;
+            }
+            case M_CASE: {
+                for (uint32_t i = 0; i < in_n; i++) {
+                    uint8_t c = in[i];
+                    if (c >= 0x80 && m.variant) return false;  // (Unicode case tables)
+                    if (m.variant == 1 && c >= 'a' && c <= 'z') c = (uint8_t)(c - 32);
+                    if (m.variant == 2 && c >= 'A' && c <= 'Z') c = (uint8_t)(c + 32);
+                    o.put(c);
+                }
+                break;
+            }
+            case M_BASE64: {
+                if (m.variant == 0) {
+                    o.put(in, in_n);
+                    break;
+                }
+                if (!mod_result_string(in, in_n, outp, t)) return false;
+                if (m.variant == 1) {
+                    o.put('"');
+                    b64_encode(mb.t, t.n, o);
+                    o.put('"');
+                    break;
+                }
+                // decode into the spare half of the output buffer, then wrap
+                OutBuf dec{outp + kModBuf / 2, 0, kModBuf / 2, true};
+                bool ok = false;
+                if (t.n % 4 == 0) ok = b64_decode(mb.t, t.n, true, dec);
+                if (!ok) {
+                    dec.n = 0;
+                    (void)b64_decode(mb.t, t.n, false, dec);
+                }
+                if (!dec.ok) return false;
+                OutBuf w{outp, 0, kModBuf / 2, true};
+                wrap_escaped(dec.p, dec.n, w);
+                if (!w.ok) return false;
+                o.n = w.n;
+                break;
+            }
+            case M_STRIP: {
+                for (uint32_t i = 0; i < in_n; i++) {
+                    const uint8_t c = in[i];
+                    if (c >= 0x80) return false;  // (unicode.IsPrint tables)
+                    if (c >= 0x20 && c != 0x7F) o.put(c);
+                }
+                break;
+            }
+            default: return false;
+        }
+        if (!o.ok) return false;
+        in = outp;
+        in_n = o.n;
+    }
+    return mod_parse(in, in_n, mb.t, rdoc, rv);
+}
+
+}  // namespace ajx

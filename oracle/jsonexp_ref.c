@@ -23,6 +23,9 @@ typedef struct {
     or_regex* re;     /* matches: compiled once */
     int static_state; /* -1 none, OR_E = static error, OR_UNSUPPORTED */
     char err[256];
+    size_t base_len;  /* the selector's plain path (before a modifier chain) */
+    or_mod mods[8];   /* pkg/json/json.go modifiers applied to the path's value */
+    int n_mods;
 } pat_entry;
 
 struct or_ruleset {
@@ -46,7 +49,14 @@ or_ruleset* or_ruleset_new(const or_pattern* patterns, uint32_t n_patterns, cons
         pat_entry* e = &rs->pats[i];
         e->p = patterns[i];
         e->static_state = -1;
-        if (or_path_supported(e->p.selector, e->p.selector_len) != 0) {
+        e->base_len = e->p.selector_len;
+        int mr = or_mod_split(e->p.selector, e->p.selector_len, &e->base_len, e->mods, 8, &e->n_mods);
+        if (mr <= 0) {
+            or_mods_free(e->mods, e->n_mods);
+            e->n_mods = 0;
+            e->base_len = e->p.selector_len;
+        }
+        if (mr < 0 || or_path_supported(e->p.selector, e->base_len) != 0) {
             e->static_state = OR_UNSUPPORTED;
             snprintf(e->err, sizeof e->err, "unsupported selector syntax");
             continue;
@@ -69,8 +79,10 @@ or_ruleset* or_ruleset_new(const or_pattern* patterns, uint32_t n_patterns, cons
 
 void or_ruleset_free(or_ruleset* rs) {
     if (!rs) return;
-    for (uint32_t i = 0; i < rs->n_pats; i++)
+    for (uint32_t i = 0; i < rs->n_pats; i++) {
         if (rs->pats[i].re) or_regex_free(rs->pats[i].re);
+        or_mods_free(rs->pats[i].mods, rs->pats[i].n_mods);
+    }
     free(rs->pats);
     free(rs->nodes);
     free(rs);
@@ -81,6 +93,7 @@ const char* or_pattern_error(or_ruleset* rs, uint32_t i) { return rs->pats[i].er
 typedef struct {
     or_result v, item;
     or_buf s;
+    or_buf mt; /* modifier chain output text (v points into it) */
 } scratch;
 
 static int str_eq(const or_buf* b, const char* v, uint32_t n) {
@@ -90,7 +103,12 @@ static int str_eq(const or_buf* b, const char* v, uint32_t n) {
 static int pattern_matches(or_ruleset* rs, uint32_t i, const char* json, size_t jlen, scratch* sc) {
     pat_entry* e = &rs->pats[i];
     if (e->static_state >= 0) return e->static_state;
-    or_gjson_get(json, jlen, e->p.selector, e->p.selector_len, &sc->v);
+    or_gjson_get(json, jlen, e->p.selector, e->base_len, &sc->v);
+    /* gjson pipes a found value (raw JSON) through the modifiers and Parses the output */
+    if (e->n_mods && sc->v.raw_len > 0) {
+        if (or_mod_apply(e->mods, e->n_mods, sc->v.raw, sc->v.raw_len, &sc->mt) != 0) return OR_UNSUPPORTED;
+        if (or_parse(sc->mt.p ? sc->mt.p : "", sc->mt.n, &sc->v) != 0) return OR_UNSUPPORTED;
+    }
     switch (e->p.op) {
         case OR_OP_EQ:
         case OR_OP_NEQ: {
@@ -126,6 +144,7 @@ int or_pattern_matches(or_ruleset* rs, uint32_t i, const char* json, size_t jlen
     or_result_free(&sc.v);
     or_result_free(&sc.item);
     or_buf_free(&sc.s);
+    or_buf_free(&sc.mt);
     return r;
 }
 
@@ -175,6 +194,7 @@ int or_expression_matches(or_ruleset* rs, const char* json, size_t jlen, int32_t
     or_result_free(&sc.v);
     or_result_free(&sc.item);
     or_buf_free(&sc.s);
+    or_buf_free(&sc.mt);
     if (r != OR_E && r != OR_UNSUPPORTED) *err_pattern = -1;
     return r;
 }
@@ -228,6 +248,7 @@ static void* run_job(void* arg) {
     or_result_free(&sc.v);
     or_result_free(&sc.item);
     or_buf_free(&sc.s);
+    or_buf_free(&sc.mt);
     free(res);
     return NULL;
 }

@@ -72,6 +72,29 @@ void or_result_string(const or_result* r, or_buf* out);
  * (it is reset on every call). */
 int or_result_array_next(const or_result* r, size_t* cursor, or_result* item);
 
+/* ---- the reference's gjson modifiers (pkg/json/json.go:161-264; gjson_mods_ref.c) ---- */
+enum { OR_MOD_EXTRACT = 1, OR_MOD_REPLACE = 2, OR_MOD_CASE = 3, OR_MOD_BASE64 = 4, OR_MOD_STRIP = 5 };
+typedef struct {
+    int kind, variant, has_old;
+    char* a; /* extract: sep; replace: old */
+    size_t a_len;
+    char* b; /* replace: new */
+    size_t b_len;
+    uint64_t pos; /* extract */
+} or_mod;
+/* Split path into a plain base (path[0 .. *base_len)) and a modifier chain: 0 none, 1 ok,
+ * -1 a form not restated. Free the chain with or_mods_free. */
+int or_mod_split(const char* path, size_t n, size_t* base_len, or_mod* mods, int max_mods, int* n_mods);
+void or_mods_free(or_mod* mods, int n);
+/* Run the chain on a found value's raw JSON: the last output text (0), or -1 undecided
+ * (non-ASCII text under @case / @strip, a Parse the oracle does not restate). */
+int or_mod_apply(const or_mod* mods, int n_mods, const char* raw, size_t raw_len, or_buf* text);
+/* gjson.Parse(text) (0; -1 for a leading '+' 'i' 'I' 'N' or NaN-like 'n'). */
+int or_parse(const char* text, size_t n, or_result* r);
+/* gjson.Get with a modifier chain (text: the chain's output, r points into it): 0, -1
+ * unsupported path, -2 undecided. */
+int or_gjson_get_mods(const char* json, size_t jlen, const char* path, size_t plen, or_result* r, or_buf* text);
+
 /* gjson's unescape(): JSON string escapes -> bytes (exact quirks restated). */
 void or_unescape(const char* s, size_t n, or_buf* out);
 

@@ -64,6 +64,9 @@ def lib():
         L = C.CDLL(path)
         L.or_gjson_get.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(_Result)]
         L.or_gjson_get.restype = C.c_int
+        L.or_gjson_get_mods.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(_Result),
+                                        C.POINTER(_Buf)]
+        L.or_gjson_get_mods.restype = C.c_int
         L.or_result_string.argtypes = [C.POINTER(_Result), C.POINTER(_Buf)]
         L.or_result_array_next.argtypes = [C.POINTER(_Result), C.POINTER(C.c_size_t), C.POINTER(_Result)]
         L.or_result_array_next.restype = C.c_int
@@ -116,6 +119,28 @@ def gjson_get(doc, path) -> Tuple[int, bytes, bytes]:
     out = (r.type, C.string_at(r.raw, r.raw_len) if r.raw_len else b"", _buf_bytes(b))
     L.or_buf_free(C.byref(b))
     L.or_result_free(C.byref(r))
+    return out
+
+
+def gjson_string_mods(doc, path):
+    """String() of gjson.Get(doc, path) for a path with the reference's modifiers
+    (gjson_mods_ref.c); None when undecided (non-ASCII text under @case / @strip)."""
+    L = lib()
+    d, p = _b(doc), _b(path)
+    r = _Result()
+    text = _Buf()
+    rc = L.or_gjson_get_mods(d, len(d), p, len(p), C.byref(r), C.byref(text))
+    if rc == -1:
+        L.or_buf_free(C.byref(text))
+        raise ValueError(f"oracle: unsupported selector {path!r}")
+    out = None
+    if rc == 0:
+        b = _Buf()
+        L.or_result_string(C.byref(r), C.byref(b))
+        out = _buf_bytes(b)
+        L.or_buf_free(C.byref(b))
+    L.or_result_free(C.byref(r))
+    L.or_buf_free(C.byref(text))
     return out
 
 

@@ -12,6 +12,9 @@ Sources (paths relative to the reference tree):
   pkg/service/auth_pipeline_test.go:389-495 `when` conditions on path "/operation"
   pkg/service/auth_pipeline_test.go:583-596 Authorization JSON of NewAuthorizationJSON
   pkg/json/json_test.go:174-181             bool stringification, escaped-dot key
+  pkg/json/json_test.go:165-187,207-263     the custom gjson modifiers (@extract @replace
+      @case @base64 @strip, chains through '|'): each gjson.Get(..).String() expectation
+      becomes an eq pattern that must be T (and a wrong value that must be F)
   tests/v1beta2/authconfig.yaml:9-17,131-150  e2e patterns (matches ^/admin(/.*)?$, eq 'true')
 
 The Go encoding/json output for the AttributeContext document is reproduced by hand:
@@ -154,6 +157,37 @@ add(JSON_TEST_DOC, P("auth.identity.email_verified", "eq", "true"), "T", src + "
 add(JSON_TEST_DOC, P("auth.identity.github\\.com", "eq", "https://github.com/john"), "T",
     src + ":177-178 (escaped dot in key)")
 add(JSON_TEST_DOC, P("auth.identity.username", "eq", "john"), "T", src + ":162-163")
+
+SA_DOC = '{"auth":{"identity":{"serviceaccount":{"name":"my:ns:sa","long-name":"SA in the NS namespace"}}}}'
+NAME_DOC = '{"auth":{"identity":{"fullname":"John Doe"}}}'
+B64_UNPADDED = '{"auth":{"identity":{"username":{"encoded":"am9obg","decoded":"john"}}}}'
+B64_PADDED = '{"auth":{"identity":{"username":{"encoded":"am9obg==","decoded":"john"}}}}'
+B64_QUOTES = ('{"auth":{"identity":{"username":{"encoded":"bXkgbmFtZSBpcyAiam9obiI=",'
+              '"decoded":"my name is \\"john\\""}}}}')
+STRIP_DOC = "{\"auth\":{\"identity\":{\"username\": \"\n\nbob\u0012\"}}}"
+MODIFIER_CASES = [
+    (JSON_TEST_DOC, "auth.identity.username.@case:upper", "JOHN", ":165-166"),
+    (JSON_TEST_DOC, 'auth.identity.email.@extract:{"sep":"@","pos":1}', "test", ":168-169"),
+    (JSON_TEST_DOC, 'auth.identity.github\\.com|@extract:{"sep":"/","pos":3}|@case:upper', "JOHN", ":180-181"),
+    (SA_DOC, "auth.identity.serviceaccount.long-name.@extract", "SA", ":210"),
+    (SA_DOC, 'auth.identity.serviceaccount.long-name.@extract:{"pos":0}', "SA", ":211"),
+    (SA_DOC, 'auth.identity.serviceaccount.long-name.@extract:{"pos":8}', "", ":212"),
+    (SA_DOC, 'auth.identity.serviceaccount.name.@extract:{"sep":":","pos":1}', "ns", ":213"),
+    (NAME_DOC, 'auth.identity.fullname.@replace:{"old":"John","new":"Jane"}', "Jane Doe", ":219"),
+    (NAME_DOC, 'auth.identity.fullname.@replace:{"old":"Peter","new":"Jane"}', "John Doe", ":220"),
+    (NAME_DOC, "auth.identity.fullname.@case:upper", "JOHN DOE", ":226"),
+    (NAME_DOC, "auth.identity.fullname.@case:lower", "john doe", ":227"),
+    (B64_UNPADDED, "auth.identity.username.encoded.@base64:decode", "john", ":233"),
+    (B64_UNPADDED, "auth.identity.username.decoded.@base64:encode", "am9obg==", ":234"),
+    (B64_PADDED, "auth.identity.username.encoded.@base64:decode", "john", ":238"),
+    (B64_PADDED, "auth.identity.username.decoded.@base64:encode", "am9obg==", ":239"),
+    (B64_QUOTES, "auth.identity.username.encoded.@base64:decode", 'my name is "john"', ":243"),
+    (B64_QUOTES, "auth.identity.username.decoded.@base64:encode", "bXkgbmFtZSBpcyAiam9obiI=", ":244"),
+    (STRIP_DOC, "auth.identity.username.@strip", "bob", ":262"),
+]
+for doc, sel, val, lines in MODIFIER_CASES:
+    add(doc, P(sel, "eq", val), "T", src + lines + " (modifier)")
+    add(doc, P(sel, "eq", val + "?"), "F", src + lines + " (modifier, another value)")
 
 src = "tests/v1beta2/authconfig.yaml"
 add(PIPELINE_DOC, P("context.request.http.path", "matches", "^/admin(/.*)?$"), "F", src + ":131-137")

@@ -9,6 +9,7 @@
 
 #include "../../authorino_amd/csrc/ajx_compiler.h"
 #include "../../authorino_amd/csrc/ajx_fast.h"
+#include "../../authorino_amd/csrc/ajx_modifiers.h"
 #include "../../authorino_amd/csrc/ajx_regex.h"
 
 using namespace ajx;
@@ -50,6 +51,15 @@ int ht_eval(void* h, const uint8_t* doc_in, uint32_t len, uint8_t* res, int32_t*
         if (pats[p].state == P_OK) {
             const Selector& s = sels[pats[p].selector];
             v = gj_get(doc, len, comps + s.comp_begin, s.comp_count, lits);
+        }
+        if (pats[p].state == P_OK && sels[pats[p].selector].mod_count) {
+            static ModBufs mb;  // (the kernel's work-item scratch)
+            const uint8_t* rd;
+            ValueRef rv;
+            res[p] = apply_modifiers(blob, sels[pats[p].selector], doc, v, mb, &rd, &rv)
+                         ? eval_pattern<true>(blob, pats[p], rd, rv)
+                         : (uint8_t)V_U;
+            continue;
         }
         res[p] = eval_pattern<true>(blob, pats[p], doc, v);
     }
