@@ -361,7 +361,8 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     }
     HIP_OK(hipEventRecord(w->ev0, s));
     // kernel: the single-pass kernel (default; ajx_scan_fused); ablate 20 the lane
-    // kernel (21..24 its ablations), 1..3 single-pass ablations
+    // kernel (21..24 its ablations), 1..3 single-pass ablations, 10..12 the single-pass
+    // kernel in 4-, 8- or 16-wave workgroups
     bool fast_tables = !force_scan;
     for (uint32_t i = 0; i < n_sets && fast_tables; i++)
         fast_tables = (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagFastOk) != 0;
@@ -370,7 +371,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     for (uint32_t i = 0; i < n_sets; i++)
         mods = mods || reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->n_modifiers != 0;
     // capture rows kept for authjx_select_from_eval_device: one ruleset, a full kernel
-    const bool full = ablate == 0 || ablate == 20;
+    const bool full = ablate == 0 || ablate == 20 || (ablate >= 10 && ablate <= 12);
     const bool keep_rows = !force_scan && n_sets == 1 && full;
     w->rows_rs = keep_rows ? sets[0] : nullptr;
     w->rows_n = n;

@@ -154,26 +154,30 @@ class BatchCore {
             uint64_t expired = 0;
             std::vector<BatchReq*> live;
             live.reserve(batch.size());
+            std::vector<BatchReq*> late;
             for (BatchReq* r : batch) {
-                if (r->deadline_ns && now >= r->deadline_ns) {
-                    expired++;
-                    r->complete(kBatchTimedOut);
-                } else {
-                    live.push_back(r);
-                }
+                if (r->deadline_ns && now >= r->deadline_ns) late.push_back(r);
+                else live.push_back(r);
             }
+            expired = late.size();
+            if (expired) {
+                std::lock_guard<std::mutex> lock(mu_);
+                stats_.expired += expired;
+            }
+            for (BatchReq* r : late) r->complete(kBatchTimedOut);
             // AuthConfig buckets (stable: arrival order inside a bucket)
             std::stable_sort(live.begin(), live.end(),
                              [](const BatchReq* a, const BatchReq* b) { return a->rs < b->rs; });
             int rc = live.empty() ? kBatchOk : eval_(live);
-            for (BatchReq* r : live) r->complete(rc);
-            std::lock_guard<std::mutex> lock(mu_);
-            stats_.expired += expired;
-            if (!live.empty()) {
-                stats_.batches++;
-                stats_.requests += live.size();
-                stats_.max_batch_seen = std::max<uint64_t>(stats_.max_batch_seen, live.size());
+            {  // counted before the callers wake, so a caller that returns sees its batch
+                std::lock_guard<std::mutex> lock(mu_);
+                if (!live.empty()) {
+                    stats_.batches++;
+                    stats_.requests += live.size();
+                    stats_.max_batch_seen = std::max<uint64_t>(stats_.max_batch_seen, live.size());
+                }
             }
+            for (BatchReq* r : live) r->complete(rc);
         }
     }
 

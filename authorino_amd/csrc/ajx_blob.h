@@ -49,10 +49,12 @@ struct Component {
 };
 
 struct Selector {
-    uint32_t comp_begin;
-    uint32_t comp_count;
-    uint32_t mod_begin;  // gjson modifiers applied to the path's value (Modifier records)
-    uint32_t mod_count;
+    // 8 B (u16 fields: the compiler caps components and modifiers at 65535), so that the
+    // LDS-staged blob stays small (it shares a CU's 160 KiB with the window rings)
+    uint16_t comp_begin;
+    uint16_t comp_count;
+    uint16_t mod_begin;  // gjson modifiers applied to the path's value (Modifier records)
+    uint16_t mod_count;
 };
 
 // The reference's custom gjson modifiers (pkg/json/json.go:161-264, registered at
@@ -125,6 +127,7 @@ struct TrieChild {
     int32_t array_index;   // -1 never matches an element
     uint32_t node;
 };
+static_assert(sizeof(Selector) == 8, "Selector layout");
 static_assert(sizeof(TrieChild) == 24, "TrieChild layout");
 static_assert(sizeof(TrieNode) == 8, "TrieNode layout");
 

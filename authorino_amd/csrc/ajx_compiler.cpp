@@ -541,7 +541,8 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             std::string base = sel;
             std::vector<ModSpec> mspec;
             const int mr = split_modifiers(sel, &base, &mspec);
-            if (mr < 0 || !split_selector(base, &pc)) {
+            if (mr < 0 || !split_selector(base, &pc) || comps.size() + pc.size() > 0xFFFFu ||
+                mods.size() + mspec.size() > 0xFFFFu) {
                 p.state = P_UNSUPPORTED;
                 out->pattern_status[i] = AUTHJX_PAT_UNSUPPORTED;
                 out->pattern_error[i] = "selector syntax not compiled for the device";
@@ -549,10 +550,10 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 continue;
             }
             Selector s;
-            s.comp_begin = (uint32_t)comps.size();
-            s.comp_count = (uint32_t)pc.size();
-            s.mod_begin = (uint32_t)mods.size();
-            s.mod_count = (uint32_t)mspec.size();
+            s.comp_begin = (uint16_t)comps.size();
+            s.comp_count = (uint16_t)pc.size();
+            s.mod_begin = (uint16_t)mods.size();
+            s.mod_count = (uint16_t)mspec.size();
             for (const ModSpec& m : mspec) {
                 Modifier r;
                 std::memset(&r, 0, sizeof r);

@@ -198,12 +198,30 @@ __device__ __forceinline__ const uint8_t* stage_blob(const uint8_t* gblob) {
 // the work-item's 128-B window ring in dynamic LDS: [blob copy (SHARED)] [ring: per wave
 // 8 chunks x 64 lanes x 16 B]
 constexpr uint32_t kWinRingBytesPerWave = 8 * 64 * 16;
-// single-pass workgroups of up to 8 waves: one LDS copy of the ruleset blob per 8 waves,
-// so blob + rings of 16 waves fit a CU's 160 KiB for blobs up to ~16 KiB (4 waves/SIMD)
+// single-pass workgroups of 4, 8 or 16 waves (fast_block): one LDS copy of the ruleset
+// blob per workgroup next to its waves' rings, so 16 waves per CU fit the 160 KiB for
+// blobs up to ~8 KiB in 4-wave groups, ~16 KiB in 8-wave groups, ~32 KiB in one 16-wave
+// group (4 waves/SIMD by registers either way)
 constexpr uint32_t kFastBlock = 512;
+constexpr uint32_t kFastMaxBlock = 1024;
 #ifndef AJX_FAST_WAVES
 #define AJX_FAST_WAVES 4  // waves per SIMD the single-pass kernels' register budget is set for
 #endif
+// the workgroup size that fits the most waves per CU for a staged blob of `blob_bytes`
+// (0: nothing staged); the smallest such size on a tie: a workgroup retires as a unit, so
+// smaller ones leave fewer idle waves behind the longest document (measured: c2 4-wave
+// 2.03 ms vs 8-wave 2.11; c3 at 16 waves/CU 2 x 8-wave 3.78 vs 1 x 16-wave 4.03)
+static uint32_t fast_block(uint32_t blob_bytes) {
+    const uint32_t stage = (blob_bytes + 15u) & ~15u;
+    uint32_t best = 0, best_w = 0;
+    for (uint32_t b = 256; b <= kFastMaxBlock; b *= 2) {
+        const uint32_t lds = stage + (b / 64) * kWinRingBytesPerWave;
+        uint32_t w = lds <= 160u * 1024u ? (160u * 1024u / lds) * (b / 64) : 0u;
+        if (w > 4u * AJX_FAST_WAVES) w = 4u * AJX_FAST_WAVES;
+        if (w > best_w) best = b, best_w = w;
+    }
+    return best ? best : 256u;
+}
 __device__ __forceinline__ WinRing lane_ring(uint32_t ring_off) {
     extern __shared__ uint4 s_dyn_ring[];
     WinRing r;
@@ -277,7 +295,7 @@ __device__ __forceinline__ bool finish_request(uint32_t r, const uint8_t* blob, 
 // Stage A alone (profiling split / ablations): structural scan -> capture rows.
 // MODE 1/2 are the loads-only / loads+classification ablations.
 template <int MODE, bool SHARED>
-__global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
+__global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fast(const uint8_t* const* __restrict__ sets,
                                                      const uint32_t* __restrict__ set_of_req,
                                                      const uint8_t* __restrict__ arena,
                                                      const uint64_t* __restrict__ offs,
@@ -296,7 +314,7 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fast(cons
 
 // Stage B alone (profiling split): patterns on the captured values, bitmap, fold
 template <bool SHARED>
-__global__ __launch_bounds__(kFastBlock) void ajx_patterns(const uint8_t* const* __restrict__ sets,
+__global__ __launch_bounds__(kFastMaxBlock) void ajx_patterns(const uint8_t* const* __restrict__ sets,
                                                     const uint32_t* __restrict__ set_of_req,
                                                     const uint8_t* __restrict__ arena,
                                                     const uint64_t* __restrict__ offs, uint32_t n,
@@ -315,7 +333,7 @@ __global__ __launch_bounds__(kFastBlock) void ajx_patterns(const uint8_t* const*
 // request's value bytes are still in cache (a separate stage-B launch re-reads them
 // from HBM). Requests stage A can not prove gjson-equivalent go to the slow list.
 template <bool SHARED>
-__global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
+__global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
                                                       const uint32_t* __restrict__ set_of_req,
                                                       const uint8_t* __restrict__ arena,
                                                       const uint64_t* __restrict__ offs,
@@ -692,7 +710,8 @@ hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist
 // gjson.Get per pattern selector (the response / header selectors of SURVEY.md §8 a14):
 // one work-item per request, the exact device Get (gj_get) for each of the ruleset's
 // patterns; out[r * stride + p] = {start (relative to the document), len, type, esc}.
-// An UNSUPPORTED selector reports type 0xFF.
+// An UNSUPPORTED selector, and one with modifiers (its value is not a span of the
+// document), reports type 0xFF.
 __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* __restrict__ sets,
                                                          const uint32_t* __restrict__ set_of_req,
                                                          const uint8_t* __restrict__ arena,
@@ -721,7 +740,7 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
     for (uint32_t q = 0; q < np; q++) {
         const uint32_t p = p0 + q;
         uint32_t* o = out + ((size_t)r * stride + q) * 3;
-        if (pats[p].state == P_UNSUPPORTED) {
+        if (pats[p].state == P_UNSUPPORTED || sels[pats[p].selector].mod_count) {
             o[0] = 0;
             o[1] = 0;
             o[2] = 0xFFu;
@@ -757,7 +776,7 @@ hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_
     if (n == 0) return hipSuccess;
     if (d_rows) {  // stage A of the single-pass kernel captures every selector's span
         const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
-        const uint32_t fblock = shared && shared_blob_bytes <= 8192 ? 256u : kFastBlock;
+        const uint32_t fblock = shared ? fast_block(shared_blob_bytes) : kFastBlock;
         const uint32_t fgrid = (n + fblock - 1) / fblock;
         const uint32_t ring_off = shared ? (shared_blob_bytes + 15u) & ~15u : 0u;
         const uint32_t lds = ring_off + (fblock / 64) * kWinRingBytesPerWave;
@@ -824,9 +843,14 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             int mode, const uint32_t* d_perm, bool mods) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
-    // small blobs: 4-wave groups (measured faster on c2); larger ones share one copy per
-    // 8 waves (c3)
-    const uint32_t block = shared && shared_blob_bytes <= 8192 ? 256u : kFastBlock;
+    // workgroup size by the waves a CU holds (each workgroup stages its own blob copy)
+    uint32_t block = shared ? fast_block(shared_blob_bytes) : kFastBlock;
+    if (mode >= 10 && mode <= 12) {  // profiling: the default kernel at a forced workgroup size
+        block = 256u << (mode - 10);
+        mode = 0;
+        if (((shared ? (shared_blob_bytes + 15u) & ~15u : 0u) + (block / 64) * kWinRingBytesPerWave) > 160u * 1024u)
+            return hipErrorInvalidValue;
+    }
     const uint32_t grid = (n + block - 1) / block;
     // dynamic LDS of the single-pass kernels: [blob copy (shared)] [window rings]
     const uint32_t ring_off = shared ? (shared_blob_bytes + 15u) & ~15u : 0u;

@@ -10,6 +10,15 @@ the `when` gates and the authorization phase, batched over many requests.
                                    priority evaluated, the first failure is PERMISSION_DENIED
                                    (:478-481); a success stores the object under
                                    auth.authorization.<name> for later priorities (:312).
+  evaluator cache                  authorization.go:56-76 (authorino_amd.cache): the key is
+                                   resolved on the device for every request whose `when`
+                                   passed; a hit grants without the rules, a success is
+                                   stored. Requests of a batch see the cache in batch order
+                                   (what serving them one after another would give).
+  denyWith (Unauthorized)          auth_pipeline.go:478-481 + customizeDenyWith :581-608:
+                                   code -> status, message / body / headers resolved on the
+                                   device against the document the denial was decided on
+                                   and stringified (json.StringifyJSON).
   response phase                   auth_pipeline.go:324-349 + :490-494 (only after a
                                    successful authorization phase): per priority, each
                                    response config's `when`, then Plain / DynamicJSON
@@ -32,13 +41,14 @@ deny or not, is the same either way).
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Callable, Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import jsonexp
 from .authorization import JSONPatternMatching, UnauthorizedError
-from .response import ResponseConfig, ResponseSelectors, wrap_responses
+from .cache import EvaluatorCache, is_hit
+from .response import JSONValue, ResponseConfig, ResponseSelectors, ValueSelectors, stringify_json, wrap_responses
 
 UNMATCHING_CONDITIONS = "unmatching conditions for config"
 CODE_OK = 0  # rpc.OK
@@ -75,6 +85,20 @@ class AuthorizationConfig:
     rules: Optional[jsonexp.Expression] = None  # JSONPatternMatching.Rules
     conditions: Optional[jsonexp.Expression] = None  # `when`
     priority: int = 0
+    cache: Optional[EvaluatorCache] = None  # AuthorizationConfig.Cache (authorization.go:56-76)
+
+
+@dataclass
+class DenyWithValues:
+    """evaluators.DenyWithValues (pkg/evaluators/config.go:70-80)."""
+
+    code: int = 0
+    message: Optional[JSONValue] = None
+    headers: List[Tuple[str, JSONValue]] = field(default_factory=list)  # []json.JSONProperty
+    body: Optional[JSONValue] = None
+
+    def values(self) -> List[JSONValue]:
+        return [v for v in [self.message, self.body] + [h for _, h in self.headers] if v is not None]
 
 
 @dataclass
@@ -84,6 +108,7 @@ class AuthConfig:
     conditions: Optional[jsonexp.Expression] = None  # AuthConfig-level `when`
     authorization: List[AuthorizationConfig] = field(default_factory=list)
     response: List[ResponseConfig] = field(default_factory=list)
+    unauthorized: Optional[DenyWithValues] = None  # AuthConfig.Unauthorized (denyWith)
 
 
 @dataclass
@@ -99,6 +124,9 @@ class AuthResult:
     # routes it to its own evaluator. The other requests of the batch are unaffected.
     undecided: bool = False
     authorization: Dict[str, object] = field(default_factory=dict)
+    status: int = 0  # denyWith code (envoy HTTP status); 0 = the gRPC code's default
+    body: str = ""   # denyWith body
+    deny_headers: List[Dict[str, str]] = field(default_factory=list)  # denyWith headers
     headers: Dict[str, str] = field(default_factory=dict)      # success: WrapResponses headers
     metadata: Dict[str, object] = field(default_factory=dict)  # success: dynamic metadata
 
@@ -148,6 +176,13 @@ class AuthPipelineBatch:
             for v in c.values():
                 if any(p.startswith("auth.authorization") or p.startswith("auth.response") for p in v.paths()):
                     raise ValueError("response selectors over auth.authorization/auth.response are not batched")
+        # cache keys: one selector ruleset per priority level (the keys of its cached configs)
+        self.key_selectors = []
+        for level in self.levels:
+            keys = [c.cache.key for c in level if c.cache is not None]
+            self.key_selectors.append(ValueSelectors(keys, self.ctx, "cache keys") if keys else None)
+        dw = auth_config.unauthorized
+        self.deny_selectors = ValueSelectors(dw.values(), self.ctx, "denyWith selectors") if dw is not None else None
 
     # one launch: expression k of `exprs` on every request in `reqs`
     def _eval(self, exprs: Sequence[jsonexp.Expression], reqs: np.ndarray, arena, offs, lens):
@@ -228,6 +263,11 @@ class AuthPipelineBatch:
                 keep = set_aside(tri)
                 tri, err = tri[:, keep], err[:, keep]
             col = {id(e): j for j, e in enumerate(exprs)}
+            keys = self.key_selectors[li]
+            und_key = np.zeros(len(live), dtype=bool)
+            if keys is not None:
+                kspans = self._spans(keys, docs, live)
+                und_key = self._set_aside_spans(kspans, live, results)
             denied = np.zeros(len(live), dtype=bool)
             for c in level:
                 # evaluator-level `when` (auth_pipeline.go:120-125): not met -> ignored
@@ -238,8 +278,16 @@ class AuthPipelineBatch:
                 else:
                     r_tri = tri[col[id(c.rules)]]
                     r_t = r_tri == runtime.T
-                for j in np.nonzero(ok_cond)[0]:
+                for j in np.nonzero(ok_cond & ~und_key)[0]:
                     i = live[j]
+                    if c.cache is not None:
+                        key = keys.value(c.cache.key, docs[i], kspans[j])  # ResolveKeyFor
+                        hit = c.cache.get(key)
+                        if is_hit(hit):  # authorization.go:61-65: the evaluator is not called
+                            results[i].authorization[c.name] = hit
+                            continue
+                        if r_t[j]:
+                            c.cache.set(key, True)  # authorization.go:70-74
                     if r_t[j]:
                         results[i].authorization[c.name] = True  # json.go:26 -> setAuthorizationObj
                     elif not denied[j]:
@@ -251,10 +299,58 @@ class AuthPipelineBatch:
                             res.message = sets[col[id(c.rules)]].pattern_error(int(err[col[id(c.rules)]][j]))
                         else:
                             res.message = str(UnauthorizedError())
-            live = live[~denied]
+            live = live[~(denied | und_key)]
+        if self.deny_selectors is not None:
+            self._deny_with(results, docs)
         if self.selectors is not None and len(live):
             self._responses(results, docs, live, arena, offs, lens)
         return results
+
+    def _spans(self, sel: ValueSelectors, docs, idx) -> np.ndarray:
+        """The selector spans of docs[idx] (one device select launch)."""
+        sub = [docs[i] for i in np.asarray(idx).tolist()]
+        lens = np.fromiter((len(d) for d in sub), dtype=np.uint32, count=len(sub))
+        offs = np.zeros(len(sub), dtype=np.uint64)
+        if len(sub):
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        arena = np.frombuffer(b"".join(sub) + b"\0", dtype=np.uint8)
+        return sel.resolve(sub, arena, offs, lens)
+
+    @staticmethod
+    def _set_aside_spans(spans, idx, results) -> np.ndarray:
+        """Requests whose selector spans the device left unresolved (type 255) become
+        undecided; returns that mask over idx."""
+        und = ((spans[:, :, 2] & 0xFF) == 255).any(axis=1) if spans.size else np.zeros(len(idx), dtype=bool)
+        for i in np.asarray(idx)[und].tolist():
+            results[i].undecided = True
+            results[i].code = CODE_UNKNOWN
+            results[i].message = UNDECIDED_MESSAGE
+            results[i].authorization = {}
+        return und
+
+    def _deny_with(self, results, docs):
+        """customizeDenyWith(result, AuthConfig.Unauthorized) (auth_pipeline.go:581-608) for
+        the requests the authorization phase denied."""
+        dw = self.config.unauthorized
+        idx = np.array([i for i, r in enumerate(results) if r.code == CODE_PERMISSION_DENIED], dtype=np.int64)
+        if not len(idx):
+            return
+        if dw.code:
+            for i in idx.tolist():
+                results[i].status = dw.code
+        sel = self.deny_selectors
+        spans = self._spans(sel, docs, idx)
+        und = self._set_aside_spans(spans, idx, results)
+        for j, i in enumerate(idx.tolist()):
+            if und[j]:
+                continue
+            r, doc = results[i], docs[i]
+            if dw.message is not None:
+                r.message = stringify_json(sel.value(dw.message, doc, spans[j]))
+            if dw.body is not None:
+                r.body = stringify_json(sel.value(dw.body, doc, spans[j]))
+            if dw.headers:
+                r.deny_headers = [{name: stringify_json(sel.value(v, doc, spans[j]))} for name, v in dw.headers]
 
     def _responses(self, results, docs, live, arena_all, offs_all, lens_all):
         """Phase 4 for the requests that passed authorization (auth_pipeline.go:490-494)."""

@@ -482,23 +482,24 @@ class ResponseConfig:
         return go_sprint_v(obj)
 
 
-class ResponseSelectors:
-    """Every gjson path of a list of response configs compiled into one selector ruleset
-    (the reconcile-time compile point), resolved per batch on the device."""
+class ValueSelectors:
+    """Every gjson path of a list of JSONValues compiled into one selector ruleset (the
+    reconcile-time compile point), resolved per batch on the device (one span per path and
+    request); value() is JSONValue.ResolveFor on those spans (pkg/json/json.go:41-53)."""
 
-    def __init__(self, configs: Sequence[ResponseConfig], ctx):
+    def __init__(self, values: Sequence[JSONValue], ctx, what: str = "selectors"):
         from . import jsonexp
 
-        self.configs = list(configs)
         self.ctx = ctx
         self.paths: List[str] = []
         self._slot: Dict[str, int] = {}
-        for c in self.configs:
-            for v in c.values():
-                for p in v.paths():
-                    if p not in self._slot:
-                        self._slot[p] = len(self.paths)
-                        self.paths.append(p)
+        for v in values:
+            if v is None:
+                continue
+            for p in v.paths():
+                if p not in self._slot:
+                    self._slot[p] = len(self.paths)
+                    self.paths.append(p)
         self.ruleset = None
         if self.paths:
             pats = [(p, int(jsonexp.EqualOperator), "") for p in self.paths]
@@ -507,13 +508,16 @@ class ResponseSelectors:
             if bad:
                 from .runtime import AuthjxError
 
-                raise AuthjxError(f"response selectors not compiled for the device: {bad}")
+                raise AuthjxError(f"{what} not compiled for the device: {bad}")
 
     def resolve(self, docs: Sequence[bytes], arena, offs, lens) -> np.ndarray:
         """u32[n][n_paths][3] spans {start, len, type | esc << 8} from the device."""
         if self.ruleset is None:
             return np.zeros((len(docs), 0, 3), dtype=np.uint32)
         return self.ctx.select_host_arena([self.ruleset], arena, offs, lens)
+
+    def value(self, v: JSONValue, doc: bytes, spans_r) -> object:
+        return self._value(v, doc, spans_r)
 
     def _value(self, v: JSONValue, doc: bytes, spans_r) -> object:
         if not v.pattern:
@@ -529,6 +533,15 @@ class ResponseSelectors:
             return "".join(parts)
         st, ln, t = spans_r[self._slot[v.pattern]]
         return result_value(doc, int(st), int(ln), int(t) & 0xFF)
+
+
+class ResponseSelectors(ValueSelectors):
+    """Every gjson path of a list of response configs compiled into one selector ruleset
+    (the reconcile-time compile point), resolved per batch on the device."""
+
+    def __init__(self, configs: Sequence[ResponseConfig], ctx):
+        self.configs = list(configs)
+        super().__init__([v for c in self.configs for v in c.values()], ctx, "response selectors")
 
     def call(self, c: ResponseConfig, doc: bytes, spans_r) -> object:
         """Plain.Call / DynamicJSON.Call (plain.go, dynamic_json.go:20-31)."""

@@ -29,6 +29,8 @@ void* hw_compile(const authjx_tree* tree, int* rc) {
     return r;
 }
 void hw_free(void* h) { delete (HtRuleset*)h; }
+// the blob header's first 32 words (sizes and section offsets, for layout checks)
+void hw_header(void* h, uint32_t* out) { std::memcpy(out, ((HtRuleset*)h)->c.blob.data(), 32 * sizeof(uint32_t)); }
 int hw_lane_ok(void* h) {
     const RulesetHdr* hd = (const RulesetHdr*)((HtRuleset*)h)->c.blob.data();
     return (hd->flags & kFlagFastOk) ? 1 : 0;

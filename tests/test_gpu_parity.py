@@ -323,6 +323,50 @@ def test_c5_full_phase_on_device(ctx):
     assert 0 < n_ok < w.n
 
 
+def test_denywith_and_cache_on_device(ctx):
+    """denyWith (auth_pipeline.go:581-608) and evaluator-cache keys (authorization.go:56-76)
+    resolved by the device select kernel on C5 documents, against the same phase through
+    the oracle: status, message, body and headers of every denied request byte for byte,
+    and the cache-granted objects (tests/test_denywith_cache_host.py has the host cases)."""
+    import dataclasses
+
+    from test_pipeline_host import OracleCtx
+
+    from authorino_amd import cache as CA
+    from authorino_amd import pipeline as P
+    from authorino_amd import workloads
+    from authorino_amd.response import JSONValue
+
+    w = workloads.make("c5", n=3000, seed=57)
+    docs = [w.doc(i) for i in range(w.n)]
+
+    def config():
+        clk = lambda: 1000.0  # noqa: E731
+        authz = list(w.auth_config.authorization)
+        authz[0] = dataclasses.replace(authz[0], cache=CA.EvaluatorCache(
+            JSONValue(pattern="{auth.metadata.tenant}:{auth.identity.sub}"), 60, clock=clk))
+        authz[-1] = dataclasses.replace(authz[-1], cache=CA.EvaluatorCache(
+            JSONValue(pattern="auth.metadata.tenant"), 60, clock=clk))
+        dw = P.DenyWithValues(
+            code=302,
+            message=JSONValue(pattern="denied {auth.identity.sub} on {context.request.http.path}"),
+            body=JSONValue(pattern="auth.identity.realm_access.roles"),
+            headers=[("Location", JSONValue(pattern="https://login/?to=https://{context.request.http.host}"
+                                                    "{context.request.http.path}")),
+                     ("X-Exp", JSONValue(pattern="auth.identity.exp")),
+                     ("X-Static", JSONValue(static="s"))])
+        return dataclasses.replace(w.auth_config, authorization=authz, unauthorized=dw)
+
+    got = P.AuthPipelineBatch(config(), ctx=ctx).evaluate(docs)
+    want = P.AuthPipelineBatch(config(), ctx=OracleCtx()).evaluate(docs)
+    n_denied = 0
+    for g, o in zip(got, want):
+        assert (g.code, g.status, g.message, g.body, g.deny_headers, g.undecided, g.authorization, g.headers) == \
+               (o.code, o.status, o.message, o.body, o.deny_headers, o.undecided, o.authorization, o.headers)
+        n_denied += g.code == P.CODE_PERMISSION_DENIED
+    assert 0 < n_denied < w.n
+
+
 def test_forest_matches_single_rulesets(ctx):
     """authjx_compile_forest: every tree of the C5 phase (+ c2's rules and a tree with a
     static regex error) in one ruleset, one scan per document; per-tree results, error

@@ -67,7 +67,10 @@ class OracleCtx:
         for r in range(n):
             doc = arena[int(offs[r]):int(offs[r]) + int(lens[r])].tobytes()
             for p, path in enumerate(sets[0 if set_of_req is None else int(set_of_req[r])].paths):
-                t, st, ln = O.gjson_span(doc, path)
+                try:
+                    t, st, ln = O.gjson_span(doc, path)
+                except ValueError:  # modifiers: not a span of the document (device: 0xFF)
+                    t, st, ln = 255, 0, 0
                 out[r, p] = (st, ln, t)
         return out
 
