@@ -77,7 +77,8 @@ struct authjx_ctx {
     int no_tenant_stage = 0;  // profiling: multi-tenant batches read tables from global memory
     int force_scan = 0;
     int ablate = 0;  // profiling only: 1/2/3 reduced single-pass variants, 20 the lane kernel,
-                     // 21..24 its ablations (ajx_kernels.hip ajx_lane_eval)
+                     // 21..24 its ablations (ajx_kernels.hip ajx_lane_eval), 31 the
+                     // single-pass kernel with the event scanner (ajx_events.h) for stage A
 };
 
 namespace {
@@ -360,18 +361,19 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         if (rc != AUTHJX_OK) return rc;
     }
     HIP_OK(hipEventRecord(w->ev0, s));
-    // kernel: the single-pass kernel (default; ajx_scan_fused); ablate 20 the lane
-    // kernel (21..24 its ablations), 1..3 single-pass ablations, 10..12 the single-pass
-    // kernel in 4-, 8- or 16-wave workgroups
+    // kernel: the single-pass kernel (default; ajx_scan_fused with the token scanner);
+    // ablate 31 the same kernel with the event scanner, 20 the lane kernel (21..24 its
+    // ablations), 1..3 single-pass ablations, 10..12 the single-pass kernel in 4-, 8- or
+    // 16-wave workgroups
     bool fast_tables = !force_scan;
     for (uint32_t i = 0; i < n_sets && fast_tables; i++)
         fast_tables = (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagFastOk) != 0;
-    const bool lane = fast_tables && ablate >= 20;
+    const bool lane = fast_tables && ablate >= 20 && ablate < 30;
     bool mods = false;  // modifier chains: the exact scan's instance with text buffers
     for (uint32_t i = 0; i < n_sets; i++)
         mods = mods || reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->n_modifiers != 0;
     // capture rows kept for authjx_select_from_eval_device: one ruleset, a full kernel
-    const bool full = ablate == 0 || ablate == 20 || (ablate >= 10 && ablate <= 12);
+    const bool full = ablate == 0 || ablate == 20 || ablate == 31 || (ablate >= 10 && ablate <= 12);
     const bool keep_rows = !force_scan && n_sets == 1 && full;
     w->rows_rs = keep_rows ? sets[0] : nullptr;
     w->rows_n = n;
@@ -406,7 +408,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
             HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                          d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
                                          w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
-                                         ablate < 20 ? ablate : 0, perm, mods));
+                                         ablate < 20 || ablate == 31 ? ablate : 0, perm, mods));
         }
     }
     return batch_done(w, sets, n_sets);

@@ -15,6 +15,7 @@
 
 #include <atomic>
 
+#include "ajx_events.h"
 #include "ajx_fast.h"
 #include "ajx_lane.h"
 #include "ajx_modifiers.h"
@@ -232,7 +233,8 @@ __device__ __forceinline__ WinRing lane_ring(uint32_t ring_off) {
 }
 
 // stage A for request r: single-pass scan into its capture row (false: slow list)
-template <int MODE>
+// EV: the event scanner (ajx_events.h); otherwise ajx_fast.h's token scanner (the default)
+template <int MODE, bool EV = false>
 __device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t* d, uint32_t len, uint64_t* row,
                                              const WinRing& ring) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
@@ -241,13 +243,15 @@ __device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t*
         return false;
     }
     const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-    return scan_doc<MODE>(blob, blob_tables(blob), d, len, row, ring, [&](uint32_t b, uint32_t nblk) -> Block16 {
+    auto load = [&](uint32_t b, uint32_t nblk) -> Block16 {
         if (b < nblk) {
             const uint4 v = a4[b];
             return Block16{v.x, v.y, v.z, v.w};
         }
         return Block16{0u, 0u, 0u, 0u};
-    });
+    };
+    if constexpr (EV) return scan_doc_ev(blob, blob_tables(blob), d, len, row, ring, load);
+    else return scan_doc<MODE>(blob, blob_tables(blob), d, len, row, ring, load);
 }
 
 // the And/Or fold of every tree of the ruleset on the pattern bitmaps; a forest ruleset
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(kFastMaxBlock) void ajx_patterns(const uint8_t* con
 // The single-pass path: stage A then stage B in the same work-item, while the
 // request's value bytes are still in cache (a separate stage-B launch re-reads them
 // from HBM). Requests stage A can not prove gjson-equivalent go to the slow list.
-template <bool SHARED>
+template <bool SHARED, bool EV>
 __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
                                                       const uint32_t* __restrict__ set_of_req,
                                                       const uint8_t* __restrict__ arena,
@@ -351,7 +355,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
     if (k >= n) return;
     uint64_t* row = rows + (size_t)r * row_stride;
     const uint8_t* d = arena + offs[r];
-    if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off))) {
+    if (!scan_request<0, EV>(blob, d, lens[r], row, lane_ring(ring_off))) {
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
@@ -366,6 +370,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
 // use one ruleset copies that blob into LDS, as the uniform-ruleset kernel does, so its
 // table reads are ds_reads; a workgroup straddling two buckets reads the tables from
 // global memory. Dynamic LDS: [blob copy (up to stage_cap bytes)] [window rings].
+template <bool EV>
 __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_tenant(
     const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
@@ -386,14 +391,14 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     if (uni) {
         const uint8_t* blob = stage_blob<true>(gblob);
         if (k >= n) return;
-        if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off)) ||
+        if (!scan_request<0, EV>(blob, d, lens[r], row, lane_ring(ring_off)) ||
             !finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
             row[0] = kRowSlow;
             slow_ids[atomicAdd(slow_count, 1u)] = r;
         }
     } else {
         if (k >= n) return;
-        if (!scan_request<0>(gblob, d, lens[r], row, lane_ring(ring_off)) ||
+        if (!scan_request<0, EV>(gblob, d, lens[r], row, lane_ring(ring_off)) ||
             !finish_request(r, gblob, d, row, out_tri, out_err, out_bm, stride)) {
             row[0] = kRowSlow;
             slow_ids[atomicAdd(slow_count, 1u)] = r;
@@ -843,6 +848,9 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             int mode, const uint32_t* d_perm, bool mods) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
+    // stage A: the token scanner (ajx_fast.h); mode 31 the event scanner (ajx_events.h)
+    const bool ev = mode == 31;
+    if (mode == 31) mode = 0;
     // workgroup size by the waves a CU holds (each workgroup stages its own blob copy)
     uint32_t block = shared ? fast_block(shared_blob_bytes) : kFastBlock;
     if (mode >= 10 && mode <= 12) {  // profiling: the default kernel at a forced workgroup size
@@ -863,17 +871,23 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             reinterpret_cast<const void*>(&ajx_scan_fast<0, false>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<1, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<2, true>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused<true>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused<false>)};
+                            reinterpret_cast<const void*>(&ajx_scan_fused<true, true>),
+                            reinterpret_cast<const void*>(&ajx_scan_fused<false, true>),
+                            reinterpret_cast<const void*>(&ajx_scan_fused<true, false>),
+                            reinterpret_cast<const void*>(&ajx_scan_fused<false, false>)};
         for (const void* k : ks) {
             const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (r != hipSuccess) return r;
         }
         // (the tenant kernel also holds static LDS for __syncthreads_and: ask only for what
         // its launch uses, blob + four window rings)
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(&ajx_scan_fused_tenant),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   kMaxTenantStageBytes + 4 * kWinRingBytesPerWave);
+        for (const void* k : {reinterpret_cast<const void*>(&ajx_scan_fused_tenant<true>),
+                              reinterpret_cast<const void*>(&ajx_scan_fused_tenant<false>)}) {
+            const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     kMaxTenantStageBytes + 4 * kWinRingBytesPerWave);
+            if (r != hipSuccess) return r;
+        }
+        return hipSuccess;
     });
     if (e != hipSuccess) return e;
     if (mode == 1 || mode == 2) {  // profiling ablations of stage A (uniform ruleset only)
@@ -900,21 +914,37 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
             hipLaunchKernelGGL((ajx_patterns<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
         }
-    } else if (shared) {  // mode 0 (default): the single-pass kernel
-        hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
-                           d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                           stride, ring_off, d_perm);
+    } else if (shared) {  // the single-pass kernel (mode 0: token scanner; 31: event scanner)
+        if (ev)
+            hipLaunchKernelGGL((ajx_scan_fused<true, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
+                               d_bm, stride, ring_off, d_perm);
+        else
+            hipLaunchKernelGGL((ajx_scan_fused<true, false>), dim3(grid), dim3(block), lds, stream, d_sets,
+                               d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids,
+                               d_tri, d_err, d_bm, stride, ring_off, d_perm);
     } else if (d_set_of_req && shared_blob_bytes && shared_blob_bytes <= kMaxTenantStageBytes) {
         // multi-tenant batch: shared_blob_bytes = the largest ruleset blob of the batch;
         // 4-wave workgroups, so more of them fall inside one AuthConfig's bucket
         const uint32_t tblock = 256, tgrid = (n + tblock - 1) / tblock;
         const uint32_t toff = (shared_blob_bytes + 15u) & ~15u;
-        hipLaunchKernelGGL(ajx_scan_fused_tenant, dim3(tgrid), dim3(tblock), toff + (tblock / 64) * kWinRingBytesPerWave,
-                           stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count,
-                           d_slow_ids, d_tri, d_err, d_bm, stride, toff, d_perm);
+        if (ev)
+            hipLaunchKernelGGL(ajx_scan_fused_tenant<true>, dim3(tgrid), dim3(tblock),
+                               toff + (tblock / 64) * kWinRingBytesPerWave, stream, d_sets, d_set_of_req, d_arena,
+                               d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
+                               stride, toff, d_perm);
+        else
+            hipLaunchKernelGGL(ajx_scan_fused_tenant<false>, dim3(tgrid), dim3(tblock),
+                               toff + (tblock / 64) * kWinRingBytesPerWave, stream, d_sets, d_set_of_req, d_arena,
+                               d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
+                               stride, toff, d_perm);
+    } else if (ev) {
+        hipLaunchKernelGGL((ajx_scan_fused<false, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+                           d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
+                           stride, ring_off, d_perm);
     } else {
-        hipLaunchKernelGGL((ajx_scan_fused<false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
-                           d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
+        hipLaunchKernelGGL((ajx_scan_fused<false, false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+                           d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
                            stride, ring_off, d_perm);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -142,6 +142,11 @@ def _fast_decl():
         L.ht_eval_fast.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8),
                                    C.POINTER(C.c_int32)]
         L.ht_eval_fast.restype = C.c_int
+        L.ht_eval_ev.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8),
+                                 C.POINTER(C.c_int32), C.c_void_p]
+        L.ht_eval_ev.restype = C.c_int
+        L.ht_eval_tok.argtypes = L.ht_eval_ev.argtypes
+        L.ht_eval_tok.restype = C.c_int
         L._fast_declared = True
     return L
 
@@ -154,6 +159,19 @@ def eval_fast(hr: "HostRuleset", doc, mis: int = 0):
     err = C.c_int32(-1)
     t = L.ht_eval_fast(hr._h, d, len(d), mis, res, C.byref(err))
     return t, err.value, list(res)[: hr.n]
+
+
+def eval_ev(hr: "HostRuleset", doc, mis: int = 0, n_sel: int = 0, token_scanner: bool = False):
+    """Single-pass path with the event scanner (or the token scanner) on the host: (tri |
+    -1 slow | -2 not eligible, err, res, capture row [found, records...] or None)."""
+    L = _fast_decl()
+    d = _b(doc)
+    res = (C.c_uint8 * max(hr.n, 1))()
+    err = C.c_int32(-1)
+    row = (C.c_uint64 * (1 + max(n_sel, 64)))()
+    f = L.ht_eval_tok if token_scanner else L.ht_eval_ev
+    t = f(hr._h, d, len(d), mis, res, C.byref(err), C.cast(row, C.c_void_p))
+    return t, err.value, list(res)[: hr.n], (list(row)[: 1 + n_sel] if t >= 0 else None)
 
 
 _W = None

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../authorino_amd/csrc/ajx_compiler.h"
+#include "../../authorino_amd/csrc/ajx_events.h"
 #include "../../authorino_amd/csrc/ajx_fast.h"
 #include "../../authorino_amd/csrc/ajx_modifiers.h"
 #include "../../authorino_amd/csrc/ajx_regex.h"
@@ -148,7 +149,24 @@ extern "C" {
 // single-pass path: returns -1 when the document is handed to the exact scan, else the
 // tri-state; res[p] receives each pattern's value. `mis` places the copy at that
 // misalignment (0..15) like an arbitrary arena offset.
+static int eval_single_pass(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
+                            bool ev, uint64_t* row_out);
 int ht_eval_fast(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err) {
+    return eval_single_pass(h, doc, len, mis, res, err, false, nullptr);
+}
+// the token scanner with its capture row (row_out: 1 + n_selectors)
+int ht_eval_tok(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
+                uint64_t* row_out) {
+    return eval_single_pass(h, doc, len, mis, res, err, false, row_out);
+}
+// the same with the event scanner (ajx_events.h) for stage A; row_out (1 + n_selectors):
+// the capture row when the request stays on the single-pass path
+int ht_eval_ev(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
+               uint64_t* row_out) {
+    return eval_single_pass(h, doc, len, mis, res, err, true, row_out);
+}
+static int eval_single_pass(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
+                            bool ev, uint64_t* row_out) {
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
     const RulesetHdr* hd = (const RulesetHdr*)blob;
     if (!(hd->flags & kFlagFastOk)) return -2;
@@ -161,11 +179,14 @@ int ht_eval_fast(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_
     alignas(16) uint8_t ring_mem[128];
     std::memset(ring_mem, 0x5A, sizeof ring_mem);
     WinRing ring{ring_mem, 0u, 16u};
-    bool ok = scan_doc(blob, blob_tables(blob), d, len, row.data(), ring, [&](uint32_t b, uint32_t nblk) -> Block16 {
+    auto load = [&](uint32_t b, uint32_t nblk) -> Block16 {
         if (b < nblk) return Block16{a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
         return Block16{0, 0, 0, 0};
-    });
+    };
+    const bool ok = ev ? scan_doc_ev(blob, blob_tables(blob), d, len, row.data(), ring, load)
+                       : scan_doc(blob, blob_tables(blob), d, len, row.data(), ring, load);
     if (!ok) return -1;
+    if (row_out) std::memcpy(row_out, row.data(), row.size() * sizeof(uint64_t));
     uint64_t t[2], u[2];
     patterns_from_row(blob, d, row.data(), t, u);
     if ((u[0] & ~hd->unsupported[0]) | (u[1] & ~hd->unsupported[1])) return -1;  // a number for the exact scan
