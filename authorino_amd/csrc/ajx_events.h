@@ -39,15 +39,13 @@ enum : uint32_t { PK_QC = 1, PK_V = 2, PK_BR = 4, PK_K = 8, PK_M = 16 };
 struct EvScan : Scan {
     uint64_t mqc;    // closing quotes of the window
     uint64_t mdl;    // scalar delimiters of the window (',' and brackets outside strings)
-    uint64_t mk;     // ':' outside strings
-    uint32_t pk;     // PK_* of the previous window's last byte
-    uint32_t knext;  // the next window's first byte is ':'
-    uint32_t sq_in;  // an event string is open at the window start
+    uint64_t ke;     // closing quotes of keys among the window's events
+    uint32_t wfl;    // carried window flags: PK_* of the previous window's last byte | 32 (an
+                     // event string is open at the window start)
     uint32_t est;    // E_*
-    uint32_t done_pos;
     // the pending capture of a member value (or array element scalar) that is a string or
-    // a scalar: selector + 1 (0: none), start, string?, backslash seen
-    uint32_t pc_sel, pc_start, pc_str, pc_esc;
+    // a scalar: selector + 1 (0: none), start, bit 0 string?, bit 1 backslash seen
+    uint32_t pc_sel, pc_start, pc_fl;
 
     // document byte q (doc position): the window ring holds the current and the previous
     // window; older or later bytes come from the document in memory
@@ -63,31 +61,22 @@ struct EvScan : Scan {
         const int32_t f = (int32_t)pc_start + 1 - bpos;
         if (f >= 64) return;
         const uint64_t live = f <= 0 ? ~0ull : ~below64f((uint32_t)f);
-        const uint64_t m = (pc_str ? mqc : mdl) & live;
+        const bool str = pc_fl & 1u;
+        const uint64_t m = (str ? mqc : mdl) & live;
         const uint64_t bs = mbs & live;
         if (!m) {
-            pc_esc |= bs != 0 ? 1u : 0u;
+            pc_fl |= bs != 0 ? 2u : 0u;
             return;
         }
         const uint32_t j = ctz64f(m);
-        const uint32_t esc_ = pc_esc | ((bs & below64f(j)) != 0 ? 1u : 0u);
+        const uint32_t esc_ = ((pc_fl >> 1) & 1u) | ((bs & below64f(j)) != 0 ? 1u : 0u);
         uint32_t type = T_STRING;
-        if (!pc_str) {
+        if (!str) {
             const uint32_t c0 = byte_doc(pc_start);
             type = c0 == 't' ? T_TRUE : c0 == 'f' ? T_FALSE : c0 == 'n' ? T_NULL : T_NUMBER;
         }
-        record((int32_t)pc_sel - 1, pc_start, (uint32_t)(bpos + (int32_t)j) + (pc_str ? 1u : 0u), type,
-               pc_str ? esc_ : 0u);
+        record((int32_t)pc_sel - 1, pc_start, (uint32_t)(bpos + (int32_t)j) + (str ? 1u : 0u), type, str ? esc_ : 0u);
         pc_sel = 0;
-    }
-
-    AJX_HD void start_capture(int32_t s, uint32_t start, bool str) {
-        found |= 1ull << s;  // (first match in document order: nothing else can claim s now)
-        pc_sel = (uint32_t)s + 1u;
-        pc_start = start;
-        pc_str = str ? 1u : 0u;
-        pc_esc = 0;
-        resolve_pending();
     }
 
     // scalars: a number (a raw run gjson takes up to its delimiter) or exactly a literal
@@ -97,7 +86,7 @@ struct EvScan : Scan {
         const uint32_t L = c0 == 'f' ? 5u : 4u;
         if ((c0 != 't' && c0 != 'f' && c0 != 'n') || p + L >= n) return false;
         uint64_t w = 0;
-        for (uint32_t j = 0; j <= L; j++) w |= (uint64_t)d[p + j] << (8 * j);
+        for (uint32_t j = 0; j <= L; j++) w |= (uint64_t)byte_doc(p + j) << (8 * j);
         const uint64_t lit = c0 == 't' ? 0x65757274ull : c0 == 'f' ? 0x65736C6166ull : 0x6C6C756Eull;
         const uint32_t nb = (uint32_t)(w >> (8 * L)) & 0xFFu;
         return (w & ((1ull << (8 * L)) - 1ull)) == lit && (nb == ',' || nb == '}' || nb == ']');
@@ -110,64 +99,101 @@ struct EvScan : Scan {
         const uint32_t lc = c | 0x20u;
         const bool isQ = c == '"', isO = lc == '{', isC = lc == '}';
         const bool arrB = (c & 0x20u) == 0u;  // '[' ']'
+        const bool isKey = ((ke >> i) & 1u) != 0;
         const uint32_t start = isQ ? open_before(i) : p;
         const uint32_t prevc = start ? byte_doc(start - 1) : 0u;
-        const bool isKey = isQ && (i == 63 ? knext != 0 : ((mk >> (i + 1)) & 1u) != 0);
         const bool tarr = depth && top_is_arr();
         const bool member = isO && est == E_KEY && prevc == ':';
         // after a key, any event but its container value means the value (a string or a
         // scalar, not an event) is complete
         const uint32_t eff = est == E_KEY && !member ? E_VAL : est;
-        const bool elem = tarr && ((eff == E_ARR && prevc == '[') || (eff == E_VAL && prevc == ','));
-        const bool keyok = depth && !tarr && ((eff == E_OBJ && prevc == '{') || (eff == E_VAL && prevc == ','));
+        const bool after_comma = eff == E_VAL && prevc == ',';
+        const bool elem = tarr && ((eff == E_ARR && prevc == '[') || after_comma);
+        const bool keyok = depth && !tarr && ((eff == E_OBJ && prevc == '{') || after_comma);
         const bool closeok = depth && tarr == arrB && prevc != ',' && prevc != ':' &&
-                             (eff == E_VAL || eff == (arrB ? E_ARR : E_OBJ));
+                             (eff == E_VAL || eff == (arrB ? E_ARR : E_OBJ)) && (depth > 1 || p + 1 == n);
         const bool ok = isKey ? keyok : isO ? (member || elem || est == E_ROOT) : isC ? closeok : elem;
         if (!ok) {
             est = E_BAD;
             return;
         }
+        if (isC) {
+            close_container(p);
+            est = depth ? E_VAL : E_DONE;
+            return;
+        }
+        // the trie node of the key, or of the value that starts here (a member container:
+        // its key's node; an array element: the index child; the root: node 0)
+        uint32_t node;
         if (isKey) {
-            key_closed(p, i);  // pending = the key's trie node (kNoNode: off every path)
+            st = X_ROOT;
+            key_closed(p, i);
             if (st == X_SLOW) {  // an escaped key on a selector path
                 est = E_BAD;
                 return;
             }
-            est = E_KEY;
-            const int32_t s = leaf_sel(pending);
-            if (s >= 0) {
-                const uint32_t vb = byte_doc(p + 2);
-                if (vb != '{' && vb != '[') start_capture(s, p + 2, vb == '"');
-                // (a container value is captured by its own open event)
-            }
-            return;
+            node = pending;
+        } else {
+            node = value_node();
         }
+        const int32_t s = leaf_sel(node);
         if (isO) {
-            if (!open_container(c, p)) {
+            if (!push(c, p, node, s)) {
                 est = E_BAD;
                 return;
             }
             est = arrB ? E_ARR : E_OBJ;
             return;
         }
-        if (isC) {
-            close_container(p);
-            est = depth ? E_VAL : E_DONE;
-            done_pos = p;
-            return;
-        }
-        // an array element that is a string (event at its closing quote) or a scalar
-        const int32_t s = leaf_sel(value_node());
         if (s >= 0) {
-            if (isQ) {
-                const uint32_t lb = last_bs_before(i);
-                record(s, start, p + 1, T_STRING, (lb != ~0u && lb > start) ? 1u : 0u);
-            } else {
-                start_capture(s, p, false);
+            // a string or a scalar value of selector s: the member value after this key
+            // (a container value is captured by its own open event), or this element
+            const uint32_t vs = isKey ? p + 2 : start;
+            const uint32_t vb = isKey ? (vs < n ? byte_doc(vs) : 0u) : c;
+            if (vb != '{' && vb != '[') {
+                if (!isKey && isQ) {
+                    const uint32_t lb = last_bs_before(i);
+                    record(s, start, p + 1, T_STRING, (lb != ~0u && lb > start) ? 1u : 0u);
+                } else {
+                    found |= 1ull << s;  // (first match in document order)
+                    pc_sel = (uint32_t)s + 1u;
+                    pc_start = vs;
+                    pc_fl = vb == '"' ? 1u : 0u;
+                    resolve_pending();
+                }
             }
         }
-        element_done();
-        est = E_VAL;
+        if (!isKey) element_done();
+        est = isKey ? E_KEY : E_VAL;
+    }
+
+    // Scan::open_container with the node and leaf selector already resolved
+    AJX_HD bool push(uint32_t c, uint32_t p, uint32_t node, int32_t s) {
+        if (depth + 1 >= 63) return false;
+        depth++;
+        const uint64_t bit = 1ull << depth;
+        is_arr = c == '[' ? is_arr | bit : is_arr & ~bit;
+        const uint32_t live = node != kNoNode && tn[node].n_children ? node : kNoNode;
+        if (live != kNoNode && depth > kFastDepth) return false;
+        set_node(depth, live);
+        if (s >= 0) {
+            found |= 1ull << s;  // first match in document order wins
+            if (ncap >= 2) return false;
+            const uint32_t v = (uint32_t)s | (depth << 8), c0 = cap0, c1 = cap1, s0 = cap0_start, s1 = cap1_start;
+            cap0 = ncap == 0 ? v : c0;
+            cap0_start = ncap == 0 ? p : s0;
+            cap1 = ncap == 1 ? v : c1;
+            cap1_start = ncap == 1 ? p : s1;
+            ncap++;
+        }
+        if (c == '[' && live != kNoNode && (tn[live].flags & 1)) {
+            if (narr >= 2) return false;
+            const uint32_t a0 = arr0, a1 = arr1;
+            arr0 = narr == 0 ? depth : a0;
+            arr1 = narr == 1 ? depth : a1;
+            narr++;
+        }
+        return true;
     }
 
     // the 64 document bytes of a window (ring position of byte 0 = a, a multiple of 64;
@@ -237,17 +263,17 @@ struct EvScan : Scan {
         const uint64_t V = outside & ~(K | M | Br | mws | mb);
         mqc = qc;
         mdl = M | Br;
-        mk = K;
         // the compact-JSON rules around ':' ',' and value starts, for the whole window
         // (P(x): x at the preceding byte)
+        const uint32_t pk = wfl;
         const uint64_t PQc = (qc << 1) | (pk & PK_QC ? 1u : 0u);
         const uint64_t PV = (V << 1) | (pk & PK_V ? 1u : 0u);
         const uint64_t PBr = (Br << 1) | (pk & PK_BR ? 1u : 0u);
         const uint64_t PK = (K << 1) | (pk & PK_K ? 1u : 0u);
         const uint64_t PM = (M << 1) | (pk & PK_M ? 1u : 0u);
         const uint64_t Vs = V & ~PV;  // scalar starts
-        knext = nx0 == ':' && bp + 64 < (int32_t)n ? 1u : 0u;
-        const uint64_t KC = qc & ((K >> 1) | ((uint64_t)knext << 63));  // closing quotes of keys
+        const uint64_t knext = nx0 == ':' && bp + 64 < (int32_t)n ? 1u : 0u;
+        const uint64_t KC = qc & ((K >> 1) | (knext << 63));  // closing quotes of keys
         uint64_t bad = (mb | mws) & outside;
         bad |= K & ~PQc;
         bad |= M & ~(PQc | PV | PBr);
@@ -258,12 +284,12 @@ struct EvScan : Scan {
         // the mark from the opening quote along the string to its closing quote)
         const uint64_t SQ = oq & ~PK;
         const uint64_t s1 = instr + SQ;
-        const uint64_t s2 = s1 + (uint64_t)sq_in;
+        const uint64_t s2 = s1 + (uint64_t)((pk >> 5) & 1u);
         const uint64_t QcE = s2 & ~instr & qc;
-        sq_in = (s1 < instr || s2 < s1) ? 1u : 0u;
         bad |= KC & ~QcE;  // a member value followed by ':'
-        pk = (uint32_t)(qc >> 63) * PK_QC | (uint32_t)(V >> 63) * PK_V | (uint32_t)(Br >> 63) * PK_BR |
-             (uint32_t)(K >> 63) * PK_K | (uint32_t)(M >> 63) * PK_M;
+        ke = KC;
+        wfl = (uint32_t)(qc >> 63) * PK_QC | (uint32_t)(V >> 63) * PK_V | (uint32_t)(Br >> 63) * PK_BR |
+              (uint32_t)(K >> 63) * PK_K | (uint32_t)(M >> 63) * PK_M | ((s1 < instr || s2 < s1) ? 32u : 0u);
         if (bad) {
             est = E_BAD;
             return;
@@ -320,11 +346,10 @@ AJX_HD bool scan_doc_ev(const uint8_t* blob, const Tables& tab, const uint8_t* d
     s.in_str = s.esc = 0;
     s.cap0 = s.cap0_start = s.cap1 = s.cap1_start = s.ncap = 0;
     s.arr0 = s.arr1 = s.narr = 0;
-    s.mqc = s.mdl = s.mk = 0;
-    s.pk = s.knext = s.sq_in = 0;
+    s.mqc = s.mdl = s.ke = 0;
+    s.wfl = 0;
     s.est = E_ROOT;
-    s.done_pos = ~0u;
-    s.pc_sel = s.pc_start = s.pc_str = s.pc_esc = 0;
+    s.pc_sel = s.pc_start = s.pc_fl = 0;
 
     const uint32_t mis = (uint32_t)((uintptr_t)d & 15u);
     const uint32_t nblk = (n + mis + 15) / 16;
@@ -342,7 +367,7 @@ AJX_HD bool scan_doc_ev(const uint8_t* blob, const Tables& tab, const uint8_t* d
             nxt[j] = load(b0 + 8 + (uint32_t)j, nblk);
         }
     }
-    if (s.est != E_DONE || s.done_pos + 1 != n || s.in_str || s.pc_sel) {
+    if (s.est != E_DONE || s.in_str || s.pc_sel) {
         row[0] = kRowSlow;
         return false;
     }
