@@ -13,6 +13,7 @@ root, taking the first `*` child that holds an entry (`treeNode.get`, index.go:1
 """
 from __future__ import annotations
 
+import ctypes as C
 from typing import Dict, Iterable, List, Optional, Tuple
 
 import numpy as np
@@ -185,6 +186,79 @@ def select_sets(index: Index, hosts: Iterable[str], not_found: int = -1) -> np.n
             v = memo[h] = not_found if cfg is None else int(cfg)
         out[i] = v
     return out
+
+
+class NativeIndex:
+    """The same tree in libauthjx.so (authorino_amd/csrc/ajx_index.cpp, include/authjx.h
+    authjx_index_*): entries are ruleset ids; `lookup_batch` resolves a micro-batch of
+    hosts (with the ':port' retry) on all host threads — the batched host lookup of
+    SURVEY.md §8 f4 (pkg/index/index.go:153-174, pkg/service/auth.go:270-289)."""
+
+    def __init__(self):
+        from . import runtime
+
+        self._L = runtime.load_library()
+        h = C.c_void_p()
+        rc = self._L.authjx_index_new(C.byref(h))
+        if rc != 0:
+            raise MemoryError("authjx_index_new: %d" % rc)
+        self._h = h
+
+    def close(self):
+        if self._h:
+            self._L.authjx_index_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set(self, key: str, set_id: int, override: bool = False) -> Optional[Exception]:
+        """index.go:67-80 (the entry is the ruleset id)"""
+        b = key.encode("utf-8")
+        rc = self._L.authjx_index_set(self._h, b, len(b), int(set_id), 1 if override else 0)
+        if rc == -7:
+            return AlreadyExistsError("authconfig already exists in the index: %s" % key)
+        if rc != 0:
+            raise ValueError("authjx_index_set: %d" % rc)
+        return None
+
+    def delete_key(self, key: str, set_id: int) -> None:
+        """index.go:93-98"""
+        b = key.encode("utf-8")
+        self._L.authjx_index_delete_key(self._h, b, len(b), int(set_id))
+
+    def get(self, host: str) -> int:
+        """`lookup` (Index.Get + the ':port' retry): the ruleset id, -1 when none"""
+        b = host.encode("utf-8")
+        out = C.c_int32(-1)
+        self._L.authjx_index_get(self._h, b, len(b), C.byref(out))
+        return out.value
+
+    def lookup_batch(self, arena: np.ndarray, offs: np.ndarray, lens: np.ndarray, n_threads: int = 0) -> np.ndarray:
+        """host r = arena[offs[r] : offs[r] + lens[r]] -> ruleset id (-1: none)"""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.empty(len(lens), dtype=np.int32)
+        rc = self._L.authjx_index_lookup_batch(self._h, arena.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                               len(lens), out.ctypes.data, int(n_threads))
+        if rc != 0:
+            raise ValueError("authjx_index_lookup_batch: %d" % rc)
+        return out
+
+
+def pack_hosts(hosts: Iterable[str]):
+    """hosts -> (arena u8, offs u64, lens u32), the layout lookup_batch takes"""
+    bs = [h.encode("utf-8") for h in hosts]
+    lens = np.fromiter((len(b) for b in bs), dtype=np.uint32, count=len(bs))
+    offs = np.zeros(len(bs), dtype=np.uint64)
+    if len(bs) > 1:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    arena = np.frombuffer(b"".join(bs), dtype=np.uint8) if bs else np.zeros(0, np.uint8)
+    return arena, offs, lens
 
 
 def bucket_order(sets: np.ndarray, lens: np.ndarray) -> np.ndarray:

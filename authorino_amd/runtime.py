@@ -128,6 +128,19 @@ def load_library(path: str = LIB_PATH):
         L.authjx_batcher_eval.restype = C.c_int
         L.authjx_batcher_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 4
         L.authjx_batcher_stats.restype = C.c_int
+        L.authjx_index_new.argtypes = [C.POINTER(C.c_void_p)]
+        L.authjx_index_new.restype = C.c_int
+        L.authjx_index_free.argtypes = [C.c_void_p]
+        L.authjx_index_free.restype = None
+        L.authjx_index_set.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_int32, C.c_int]
+        L.authjx_index_set.restype = C.c_int
+        L.authjx_index_delete_key.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_int32]
+        L.authjx_index_delete_key.restype = C.c_int
+        L.authjx_index_get.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.POINTER(C.c_int32)]
+        L.authjx_index_get.restype = C.c_int
+        L.authjx_index_lookup_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                                C.c_void_p, C.c_uint32]
+        L.authjx_index_lookup_batch.restype = C.c_int
         _lib = L
         return L
 

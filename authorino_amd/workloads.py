@@ -388,6 +388,14 @@ def c4_expression(rng: np.random.Generator, tenant: int, plain, rx):
     return All(*groups)
 
 
+def c4_index_entries(n_configs: int = 10000, n_wild: int = 100):
+    """(host key, set id) of C4's AuthConfigs: t<i>.example.com, then the wildcards
+    *.r<j>.example.com"""
+    n_exact = n_configs - n_wild
+    return [("t%d.example.com" % i if i < n_exact else "*.r%d.example.com" % (i - n_exact), i)
+            for i in range(n_configs)]
+
+
 def c4_index_and_rules(n_configs: int = 10000, n_wild: int = 100, seed: int = 4):
     """The AuthConfigs: hosts t<i>.example.com (i < n_configs - n_wild) and wildcards
     *.r<j>.example.com, in a pkg/index restatement whose entries are set ids."""
@@ -397,9 +405,7 @@ def c4_index_and_rules(n_configs: int = 10000, n_wild: int = 100, seed: int = 4)
     plain, rx = _c4_pattern_pool()
     idx = Index()
     exprs = []
-    n_exact = n_configs - n_wild
-    for i in range(n_configs):
-        host = "t%d.example.com" % i if i < n_exact else "*.r%d.example.com" % (i - n_exact)
+    for host, i in c4_index_entries(n_configs, n_wild):
         err = idx.set("ns/cfg-%d" % i, host, i, False)
         assert err is None, err
         exprs.append(c4_expression(rng, i, plain, rx))

@@ -364,6 +364,23 @@ def main():
         pcie = {"value": int(rpr.sum()) / dt, "unit": "request×rule evals/s", "ms_per_batch": dt * 1e3,
                 "decisions_per_s": w.n / dt,
                 "note": "authjx_eval_batch from pageable host buffers (H2D arena copy + kernels + D2H), one GPU"}
+    if rank == 0 and world == 1 and not args.no_cpu and w.hosts is not None:
+        # c4's AuthConfig selection on the host: the native batched index
+        # lookup (authjx_index_lookup_batch) of every request's host, all host threads; not
+        # in the timed GPU step, as in the reference (pkg/service/auth.go:270-289)
+        from authorino_amd import index as hix
+
+        nat = hix.NativeIndex()
+        for key, sid in workloads.c4_index_entries():
+            nat.set(key, sid)
+        ha, ho, hl = hix.pack_hosts(w.hosts)
+        nth = host_threads()
+        got = nat.lookup_batch(ha, ho, hl, n_threads=nth)
+        t0 = time.perf_counter()
+        nat.lookup_batch(ha, ho, hl, n_threads=nth)
+        dt = time.perf_counter() - t0
+        extra["host_lookup"] = {"requests": w.n, "ms": dt * 1e3, "hosts_per_s": w.n / dt, "threads": nth,
+                                "equal_to_restatement": bool(np.array_equal(got, w.set_of_req.astype(np.int32)))}
     undecided = int((tri_h == runtime.UNDECIDED).sum())
     exact_path = ctx.last_exact_count()  # requests the single-pass kernel handed to the exact scan
 

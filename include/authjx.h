@@ -67,6 +67,7 @@ extern "C" {
 #define AUTHJX_ELIMIT (-4)
 #define AUTHJX_ETIMEDOUT (-5) /* micro-batcher: the deadline passed before evaluation */
 #define AUTHJX_ECLOSED (-6)   /* micro-batcher: destroyed while the request waited for room */
+#define AUTHJX_EEXIST (-7)    /* index: the key is taken and override was not asked for */
 
 /* jsonexp.Operator (pkg/jsonexp/expressions.go:12-19) */
 #define AUTHJX_OP_UNKNOWN 0
@@ -261,6 +262,28 @@ int authjx_batcher_eval(authjx_batcher* b, const authjx_ruleset* rs, const uint8
                         uint64_t timeout_us, uint8_t* out_tristate, int32_t* out_err_idx);
 int authjx_batcher_stats(authjx_batcher* b, uint64_t* batches, uint64_t* requests, uint64_t* expired,
                          uint64_t* max_batch_seen);
+
+/* ---- AuthConfig index (host) ----------------------------------------------------
+ * pkg/index/index.go's authConfigTree (:37-243), native, for the micro-batcher's
+ * per-request AuthConfig selection (config C4). Keys are hostnames ('*' labels are
+ * wildcards); entries are ruleset ids (the `set_of_req` values of authjx_eval_batch).
+ * Set = index.go:67-80 (AUTHJX_EEXIST: "authconfig already exists in the index" when the
+ * key is taken and override is 0); DeleteKey = :93-98 (the key's entry is removed only
+ * when it is this id's). Lookups take a shared lock, Set/DeleteKey an exclusive one
+ * (the reference's RWMutex, :51). */
+typedef struct authjx_index authjx_index;
+int authjx_index_new(authjx_index** out);
+void authjx_index_free(authjx_index* ix);
+int authjx_index_set(authjx_index* ix, const char* key, uint32_t key_len, int32_t set_id, int override_);
+int authjx_index_delete_key(authjx_index* ix, const char* key, uint32_t key_len, int32_t set_id);
+/* Index.Get (index.go:56-65) with the ':port' retry of pkg/service/auth.go:270-280:
+ * *out_set = the host's ruleset id, -1 when none (the reference answers NOT_FOUND,
+ * auth.go:282-287). */
+int authjx_index_get(const authjx_index* ix, const char* host, uint32_t host_len, int32_t* out_set);
+/* The same for a micro-batch of hosts (host r = hosts[offs[r] .. offs[r] + lens[r])) on
+ * n_threads host threads (0: all cores), each distinct host walked once per thread. */
+int authjx_index_lookup_batch(const authjx_index* ix, const uint8_t* hosts, const uint64_t* offs,
+                              const uint32_t* lens, uint32_t n, int32_t* out_sets, uint32_t n_threads);
 
 #ifdef __cplusplus
 }

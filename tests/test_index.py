@@ -119,3 +119,81 @@ def test_bucket_order_groups_by_config_then_longest_first():
     assert (np.diff(s) >= 0).all()
     same = np.diff(s) == 0
     assert (np.diff(c)[same] <= 0).all()
+
+
+# ---- the native index (authorino_amd/csrc/ajx_index.cpp, authjx_index_*) ----------------
+
+def test_native_index_reference_tree():
+    """index_test.go:38-140 on the native tree (entries are ruleset ids)"""
+    n = ix.NativeIndex()
+    assert n.set("*.io", 1) is None
+    assert n.set("talker-api.nip.io", 2) is None
+    assert n.set("*.pets.com", 2) is None
+    assert n.set("api.acme.com", 3) is None
+    assert n.set("*.acme.com", 4) is None
+    assert isinstance(n.set("talker-api.nip.io", 5), ix.AlreadyExistsError)
+    assert n.get("dogs.pets.com") == 2
+    assert n.get("api.acme.com") == 3
+    assert n.get("www.acme.com") == 4
+    assert n.get("talker-api.nip.io") == 2
+    assert n.get("foo.nip.io") == 1
+    assert n.get("foo.org") == -1
+    n.delete_key("talker-api.nip.io", 2)
+    n.delete_key("*.pets.com", 2)
+    assert n.get("talker-api.nip.io") == 1  # the wildcard above it now
+    assert n.get("dogs.pets.com") == -1
+    n.delete_key("*.acme.com", 3)  # not its id: stays
+    assert n.get("www.acme.com") == 4
+    assert n.set("talker-api.nip.io", 7, override=True) is None
+    assert n.get("talker-api.nip.io") == 7
+    assert n.get("talker-api.nip.io:8080") == 7  # the ':port' retry (auth.go:270-280)
+    assert n.get("api.acme.com:443") == 3
+
+
+def _rand_host(rng, labels):
+    k = int(rng.integers(1, 5))
+    return ".".join(labels[int(rng.integers(0, len(labels)))] for _ in range(k))
+
+
+def test_native_index_matches_restatement():
+    """random keys (wildcards, empty labels, overrides, deletes) and hosts (ports):
+    the native lookups equal index.lookup on the Python restatement"""
+    rng = np.random.default_rng(41)
+    labels = ["a", "b", "io", "com", "*", "", "api", "x-1"]
+    for _ in range(30):
+        py, nat = ix.Index(), ix.NativeIndex()
+        keys = []
+        for j in range(int(rng.integers(1, 40))):
+            key = _rand_host(rng, labels)
+            ov = bool(rng.random() < 0.3)
+            e1 = py.set("id%d" % j, key, j, ov)
+            e2 = nat.set(key, j, ov)
+            assert (e1 is None) == (e2 is None), key
+            keys.append((key, j))
+        for key, j in keys[: int(rng.integers(0, len(keys) + 1))]:
+            if rng.random() < 0.3:
+                py.delete_key("id%d" % j, key)
+                nat.delete_key(key, j)
+        hosts = [_rand_host(rng, labels) + (":%d" % rng.integers(1, 9999) if rng.random() < 0.3 else "")
+                 for _ in range(300)]
+        want = [ix.lookup(py, h) for h in hosts]
+        want = np.array([-1 if w is None else w for w in want], dtype=np.int32)
+        assert [nat.get(h) for h in hosts] == list(want)
+        a, o, ln = ix.pack_hosts(hosts)
+        for nt in (1, 3):
+            assert np.array_equal(nat.lookup_batch(a, o, ln, n_threads=nt), want)
+
+
+def test_native_index_batch_c4_hosts():
+    """the C4 host population (10k tenants + wildcards, Zipf traffic): the batched native
+    lookup equals the restatement's select_sets"""
+    from authorino_amd import workloads as W
+
+    index, nat = ix.Index(), ix.NativeIndex()
+    for key, sid in W.c4_index_entries(n_configs=2000, n_wild=50):
+        assert index.set("ns/cfg-%d" % sid, key, sid, False) is None
+        assert nat.set(key, sid) is None
+    hosts = W.c4_hosts(20000, 2000, 50, np.random.default_rng(5))
+    a, o, ln = ix.pack_hosts(hosts)
+    got = nat.lookup_batch(a, o, ln, n_threads=4)
+    assert np.array_equal(got, ix.select_sets(index, hosts).astype(np.int32))
