@@ -52,6 +52,8 @@ EXPORTS = [
     "authjx_select_from_eval_device",
     "authjx_ruleset_trees", "authjx_batcher_create", "authjx_batcher_destroy", "authjx_batcher_eval",
     "authjx_batcher_stats",
+    "authjx_index_new", "authjx_index_free", "authjx_index_set", "authjx_index_delete_key", "authjx_index_get",
+    "authjx_index_lookup_batch",
 ]
 
 
