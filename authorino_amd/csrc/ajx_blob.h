@@ -41,10 +41,15 @@ enum : uint8_t { OP_UNKNOWN = 0, OP_EQ = 1, OP_NEQ = 2, OP_INCL = 3, OP_EXCL = 4
 // fold code (op in bits 24..31, argument in bits 0..23)
 enum : uint32_t { C_OPEN_AND = 1, C_OPEN_OR = 2, C_PAT = 3, C_CLOSE = 4, C_CONST_T = 5, C_CONST_F = 6 };
 
+// Component::array_index of a last path part that is exactly "#": on an array, gjson's
+// parseArray answers the element count (Number, Raw = strconv.Itoa, at the ']'); on an
+// object the part is the key "#"
+constexpr int32_t kArrCount = -2;
+
 struct Component {
     uint32_t lit_off;     // object-key bytes (escapes removed) in the literal pool
     uint32_t lit_len;
-    int32_t array_index;  // element index when the value is an array, -1 = never
+    int32_t array_index;  // element index when the value is an array, -1 = never, kArrCount
     uint32_t hash;        // FNV-1a of the key bytes
 };
 

@@ -51,7 +51,10 @@ bool split_selector(const std::string& p, std::vector<PathComponent>* out) {
             if (i < n && (p[i] == '|' || p[i] == '#')) return false;  // special in array context
             continue;
         }
-        if (c == '|' || c == '#' || c == '*' || c == '?') return false;
+        if (c == '|' || c == '*' || c == '?') return false;
+        // '#' starts gjson's array forms: "#.key" (a JSON array of each element's key), "#("
+        // / "#[" queries — not compiled; a last part "#" is the element count (kArrCount)
+        if (c == '#' && i + 1 < n && (p[i + 1] == '.' || p[i + 1] == '(' || p[i + 1] == '[')) return false;
         if (c == '.' && i + 1 < n && (p[i + 1] == '@' || p[i + 1] == '[' || p[i + 1] == '{')) return false;
     }
     // parseObjectPath repeatedly on the remainder
@@ -81,7 +84,8 @@ bool split_selector(const std::string& p, std::vector<PathComponent>* out) {
         size_t dot = p.find('.', pos);
         std::string raw = p.substr(pos, (dot == std::string::npos ? n : dot) - pos);
         comp.key = part;
-        comp.array_index = escaped && raw.find('\\') != std::string::npos ? -1 : array_index_of(raw);
+        comp.array_index = raw == "#" ? kArrCount
+                           : escaped && raw.find('\\') != std::string::npos ? -1 : array_index_of(raw);
         out->push_back(comp);
         if (!more) break;
         pos = next;
@@ -541,7 +545,9 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             std::string base = sel;
             std::vector<ModSpec> mspec;
             const int mr = split_modifiers(sel, &base, &mspec);
-            if (mr < 0 || !split_selector(base, &pc) || comps.size() + pc.size() > 0xFFFFu ||
+            const bool ok_path = mr >= 0 && split_selector(base, &pc);
+            const bool counted = ok_path && !pc.empty() && pc.back().array_index == kArrCount;
+            if (!ok_path || (counted && !mspec.empty()) || comps.size() + pc.size() > 0xFFFFu ||
                 mods.size() + mspec.size() > 0xFFFFu) {
                 p.state = P_UNSUPPORTED;
                 out->pattern_status[i] = AUTHJX_PAT_UNSUPPORTED;
@@ -593,7 +599,9 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     std::vector<std::vector<uint16_t>> sel_pats(sels.size());
     uint64_t null_true[2] = {0, 0}, static_err[2] = {0, 0}, unsup[2] = {0, 0};
     // (modifier chains run in the exact scan only: such a ruleset has no single-pass tables)
+    // (a count selector is answered by the exact scan only)
     bool fast_ok = np <= kFastMaxPatterns && sels.size() <= kFastMaxSelectors && mods.empty();
+    for (const Component& c : comps) fast_ok = fast_ok && c.array_index != kArrCount;
     for (size_t s = 0; s < sels.size() && fast_ok; s++) {
         uint32_t cur = 0;
         for (uint32_t k = 0; k < sels[s].comp_count; k++) {

@@ -37,8 +37,11 @@ struct ValueRef {
     uint32_t start;  // raw span [start, end) in the document
     uint32_t end;
     uint8_t type;    // T_*
-    uint8_t esc;     // string contains a backslash (needs unescape)
+    uint8_t esc;     // string contains a backslash (needs unescape); kValCount: a count
 };
+// ValueRef::esc of a Number that is an array's element count (a "#" part, kArrCount):
+// not a document span — the count is in `start` (start == end)
+constexpr uint8_t kValCount = 2;
 
 // ---------------------------------------------------------------------------------
 // scanning primitives (gjson parseString / parseSquash / parseNumber / parseLiteral)
@@ -448,6 +451,16 @@ AJX_HD bool string_of(const uint8_t* d, const ValueRef& v, StrSrc* s) {
             else s->init_raw(d, v.start + 1, v.end - 1);
             return true;
         case T_NUMBER: {
+            if (v.esc == kValCount) {  // an element count: its decimal digits
+                uint32_t x = v.start, nd = 0;
+                uint8_t rev[10];
+                do { rev[nd++] = (uint8_t)('0' + x % 10u); x /= 10u; } while (x);
+                s->kind = StrSrc::S_NUM; s->bn = s->bi = 0; s->done = false; s->pos = 0;
+                s->num.kind = NumCanon::K_DIGITS; s->num.neg = 0; s->num.nd = (uint8_t)nd; s->num.dp = (int16_t)nd;
+                for (uint32_t j = 0; j < nd; j++) s->num.dig[j] = rev[nd - 1 - j];
+                s->total = (int32_t)nd;
+                return true;
+            }
             uint32_t k = v.start;
             if (k < v.end && d[k] == '-') k++;
             for (; k < v.end; k++)
@@ -619,6 +632,13 @@ AJX_HD ValueRef gj_get(const uint8_t* d, uint32_t n, const Component* comps, uin
                        ch == 'I' || ch == 'N') {
                 num = true;
             } else if (is_arr && ch == ']') {
+                if (c.array_index == kArrCount && !more) {  // parseArray: Number(h - 1) at ']'
+                    ValueRef v;
+                    v.start = v.end = (uint32_t)(fh[depth] - 1);
+                    v.type = T_NUMBER;
+                    v.esc = kValCount;
+                    return v;
+                }
                 i++;
                 if (depth == 0) return none;
                 depth--;

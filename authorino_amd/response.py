@@ -183,6 +183,11 @@ def _go_bytes_str(b: bytes) -> str:
     return b.decode("utf-8", "replace")
 
 
+# authjx_value.esc of an element count (a `#` path part; ajx_device.h kValCount): the
+# count is in `start`, not a document span
+VAL_COUNT = 2
+
+
 def result_string(doc: bytes, start: int, length: int, typ: int) -> str:
     """gjson Result.String()."""
     raw = doc[start:start + length]
@@ -529,9 +534,14 @@ class ValueSelectors:
                     parts.append(s)
                 else:
                     st, ln, t = spans_r[self._slot[s]]
-                    parts.append(result_string(doc, int(st), int(ln), int(t) & 0xFF))
+                    if int(t) >> 8 == VAL_COUNT:
+                        parts.append(str(int(st)))
+                    else:
+                        parts.append(result_string(doc, int(st), int(ln), int(t) & 0xFF))
             return "".join(parts)
         st, ln, t = spans_r[self._slot[v.pattern]]
+        if int(t) >> 8 == VAL_COUNT:  # an array's element count (a `#` part): Number
+            return float(int(st))
         return result_value(doc, int(st), int(ln), int(t) & 0xFF)
 
 

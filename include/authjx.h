@@ -195,11 +195,13 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
 #define AUTHJX_JSON_TRUE 4
 #define AUTHJX_JSON_JSON 5
 #define AUTHJX_JSON_UNSUPPORTED 255
+#define AUTHJX_VALUE_COUNT 2 /* authjx_value.esc: `start` is an array's element count (a
+                              * last path part "#", gjson parseArray), len 0: no span */
 typedef struct {
     uint32_t start;
     uint32_t len;
     uint8_t type;
-    uint8_t esc;
+    uint8_t esc; /* 1: a string with escapes (gjson unescape applies); AUTHJX_VALUE_COUNT */
     uint16_t reserved;
 } authjx_value;
 

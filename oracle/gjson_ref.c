@@ -12,6 +12,7 @@
  * byte outside a-z, parentheses counted by the squash) is kept.
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -364,7 +365,7 @@ static void parse_array_path(const char* path, size_t n, arrpath* r) {
             }
             return;
         }
-        if (path[i] == '#') r->arrch = 1; /* '#' selectors are rejected up front */
+        if (path[i] == '#') r->arrch = 1; /* ("#." and "#(" "#[" forms are rejected up front) */
     }
     r->part = path;
     r->part_len = n;
@@ -452,6 +453,19 @@ static size_t parse_array(pctx* c, size_t i, const char* path, size_t plen, int*
                     num = 1;
                     break;
                 case ']':
+                    if (rp.arrch && rp.part_len == 1 && rp.part[0] == '#') {
+                        /* the element count: Number(h - 1), Raw = strconv.Itoa(h - 1) */
+                        char dg[24];
+                        int nd = snprintf(dg, sizeof dg, "%lld", (long long)(h - 1));
+                        or_buf_reset(&c->value->own);
+                        or_buf_push(&c->value->own, dg, (size_t)nd);
+                        c->value->type = OR_NUMBER;
+                        c->value->raw = c->value->own.p;
+                        c->value->raw_len = (size_t)nd;
+                        c->value->num = (double)(h - 1);
+                        *hit_out = 1;
+                        return i + 1;
+                    }
                     *hit_out = 0;
                     return i + 1;
             }
@@ -575,7 +589,10 @@ int or_path_supported(const char* p, size_t n) {
     for (size_t i = 0; i < n; i++) {
         char c = p[i];
         if (c == '\\') { i++; if (i < n && (p[i] == '|' || p[i] == '#')) return -1; continue; }
-        if (c == '|' || c == '#' || c == '*' || c == '?') return -1;
+        if (c == '|' || c == '*' || c == '?') return -1;
+        /* '#' array forms: "#.key" lists and "#(" "#[" queries are not restated; a
+         * part "#" on an array is its element count */
+        if (c == '#' && i + 1 < n && (p[i + 1] == '.' || p[i + 1] == '(' || p[i + 1] == '[')) return -1;
         if (c == '.' && i + 1 < n && (p[i + 1] == '@' || p[i + 1] == '[' || p[i + 1] == '{')) return -1;
     }
     return 0;

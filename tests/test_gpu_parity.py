@@ -583,3 +583,39 @@ def test_pipeline_sets_aside_undecided_requests():
     assert res[0].undecided and res[0].code == pipeline.CODE_UNKNOWN
     assert not res[1].undecided and res[1].code == pipeline.CODE_OK
     assert not res[2].undecided and res[2].code == pipeline.CODE_PERMISSION_DENIED
+
+
+def test_count_selectors_on_device(ctx):
+    """`#` (array element count) selectors through the C-ABI: pattern results and
+    selected values (AUTHJX_VALUE_COUNT) against the oracle (tests/test_count_selector.py)."""
+    import fuzz_util as FU
+    from test_count_selector import rand_count_patterns
+
+    rng = np.random.default_rng(1300)
+    checked = 0
+    for _ in range(25):
+        pats = rand_count_patterns(rng, int(rng.integers(1, 6)))
+        nodes, root = FU.chain(len(pats))
+        ors = O.Ruleset(pats, nodes, root)
+        docs = [FU.rand_doc(rng) for _ in range(300)]
+        if any(ors.pattern(p, docs[0]) == O.UNSUPPORTED for p in range(len(pats))):
+            continue
+        rs = ctx.compile(pats, nodes, root)
+        tri, err, bm = ctx.eval_host([rs], docs)
+        lens = np.array([len(d) for d in docs], dtype=np.uint32)
+        offs = np.zeros(len(docs), dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1])
+        arena = np.frombuffer(b"".join(docs) + b"\0", dtype=np.uint8)
+        otri, oerr, obm = O.eval_batch([ors], arena, offs, lens)
+        assert np.array_equal(tri, otri) and np.array_equal(err, oerr) and np.array_equal(bm, obm)
+        vals = ctx.select_host_arena([rs], arena, offs, lens)
+        for r in range(0, len(docs), 7):
+            for p, (sel, _, _) in enumerate(pats):
+                st, ln, t = (int(x) for x in vals[r][p])
+                ot, _, os_ = O.gjson_get(docs[r], sel.encode())
+                if t >> 8 == 2:
+                    assert ot == O.T_NUMBER and os_ == str(st).encode(), (sel, docs[r])
+                else:
+                    assert (t & 0xFF) == ot, (sel, docs[r])
+        checked += len(docs)
+    assert checked > 3000
