@@ -8,7 +8,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libauthjx.so")
-SOURCES = ["ajx_regex.cpp", "ajx_compiler.cpp", "ajx_api.cpp", "ajx_index.cpp", "ajx_kernels.hip"]
+SOURCES = ["ajx_regex.cpp", "ajx_compiler.cpp", "ajx_api.cpp", "ajx_index.cpp", "ajx_producer.cpp", "ajx_kernels.hip"]
 HEADERS = ["ajx_blob.h", "ajx_device.h", "ajx_float.h", "ajx_modifiers.h", "ajx_batcher.h", "ajx_fast.h", "ajx_events.h", "ajx_lane.h", "ajx_regex.h", "ajx_compiler.h", "ajx_kernels.h"]
 ARCH = os.environ.get("AUTHJX_ARCH", "gfx950")
 

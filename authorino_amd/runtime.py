@@ -53,7 +53,7 @@ EXPORTS = [
     "authjx_ruleset_trees", "authjx_batcher_create", "authjx_batcher_destroy", "authjx_batcher_eval",
     "authjx_batcher_stats",
     "authjx_index_new", "authjx_index_free", "authjx_index_set", "authjx_index_delete_key", "authjx_index_get",
-    "authjx_index_lookup_batch",
+    "authjx_index_lookup_batch", "authjx_pack_json",
 ]
 
 
@@ -143,6 +143,9 @@ def load_library(path: str = LIB_PATH):
         L.authjx_index_lookup_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                                 C.c_void_p, C.c_uint32]
         L.authjx_index_lookup_batch.restype = C.c_int
+        L.authjx_pack_json.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64,
+                                       C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32]
+        L.authjx_pack_json.restype = C.c_int
         _lib = L
         return L
 

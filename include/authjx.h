@@ -287,6 +287,40 @@ int authjx_index_get(const authjx_index* ix, const char* host, uint32_t host_len
 int authjx_index_lookup_batch(const authjx_index* ix, const uint8_t* hosts, const uint64_t* offs,
                               const uint32_t* lens, uint32_t n, int32_t* out_sets, uint32_t n_threads);
 
+/* ---- Authorization JSON packing (host) -------------------------------------------
+ * The producer's output stage (pkg/service/auth_pipeline.go:542-616 GetAuthorizationJSON,
+ * json.Marshal per evaluator call in the reference): each request's values, walked once
+ * by the caller into a TAPE, are encoded with encoding/json's rules (HTML-safe string
+ * escapes, U+2028/U+2029, invalid UTF-8 as \ufffd, map keys sorted by bytes, float64 'f'
+ * or 'e' by magnitude) straight into the batch arena that authjx_eval_batch reads.
+ * Tape (little-endian), one value:
+ *   AUTHJX_TAPE_NULL / TRUE / FALSE
+ *   AUTHJX_TAPE_F64 <8 B double>      float64 (NaN / Inf: the request fails, as Marshal does)
+ *   AUTHJX_TAPE_I64 <8 B int64>       integer types
+ *   AUTHJX_TAPE_STRING <u32 len><bytes>
+ *   AUTHJX_TAPE_RAW <u32 len><bytes>  pre-encoded JSON (json.RawMessage), copied
+ *   AUTHJX_TAPE_ARRAY <u32 n><n values>
+ *   AUTHJX_TAPE_OBJECT <u32 n><n x (<u32 len><key bytes> value)>  a struct: member order kept
+ *   AUTHJX_TAPE_MAP <u32 n><same>     a map: members written sorted by key bytes */
+#define AUTHJX_TAPE_NULL 1
+#define AUTHJX_TAPE_TRUE 2
+#define AUTHJX_TAPE_FALSE 3
+#define AUTHJX_TAPE_F64 4
+#define AUTHJX_TAPE_I64 5
+#define AUTHJX_TAPE_STRING 6
+#define AUTHJX_TAPE_RAW 7
+#define AUTHJX_TAPE_ARRAY 8
+#define AUTHJX_TAPE_OBJECT 9
+#define AUTHJX_TAPE_MAP 10
+/* Request r's tape is tapes[tape_offs[r] .. + tape_lens[r]); its document goes to
+ * arena[out_offs[r] .. + out_lens[r]), the documents back to back in request order, on
+ * n_threads host threads (0: all cores). *out_total = the bytes the batch needs:
+ * AUTHJX_ELIMIT (nothing written) when that exceeds arena_cap; AUTHJX_EINVAL when a
+ * tape is malformed or holds a NaN / Inf (that request: out_offs = ~0, out_lens = 0). */
+int authjx_pack_json(const uint8_t* tapes, const uint64_t* tape_offs, const uint32_t* tape_lens, uint32_t n,
+                     uint8_t* arena, uint64_t arena_cap, uint64_t* out_offs, uint32_t* out_lens,
+                     uint64_t* out_total, uint32_t n_threads);
+
 #ifdef __cplusplus
 }
 #endif
