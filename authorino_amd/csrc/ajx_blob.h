@@ -45,6 +45,10 @@ enum : uint32_t { C_OPEN_AND = 1, C_OPEN_OR = 2, C_PAT = 3, C_CLOSE = 4, C_CONST
 // parseArray answers the element count (Number, Raw = strconv.Itoa, at the ']'); on an
 // object the part is the key "#"
 constexpr int32_t kArrCount = -2;
+// ... of a part "#" followed by more parts (gjson's alog, "friends.#.first"): on an array,
+// the JSON array of Get(element, rest) over the elements where it exists (raw values,
+// comma-joined, at the ']'); on an object the part is the key "#" and the path goes on
+constexpr int32_t kArrList = -3;
 
 struct Component {
     uint32_t lit_off;     // object-key bytes (escapes removed) in the literal pool
@@ -199,5 +203,6 @@ struct RulesetHdr {
     uint64_t unsupported[2];    // pattern p can not be decided on the device
 };
 constexpr uint32_t kFlagFastOk = 4;
+constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the exact scan's buffers
 
 }  // namespace ajx

@@ -54,11 +54,12 @@ bool split_selector(const std::string& p, std::vector<PathComponent>* out) {
         if (c == '|' || c == '*' || c == '?') return false;
         // '#' starts gjson's array forms: "#.key" (a JSON array of each element's key), "#("
         // / "#[" queries — not compiled; a last part "#" is the element count (kArrCount)
-        if (c == '#' && i + 1 < n && (p[i + 1] == '.' || p[i + 1] == '(' || p[i + 1] == '[')) return false;
+        if (c == '#' && i + 1 < n && (p[i + 1] == '(' || p[i + 1] == '[')) return false;
         if (c == '.' && i + 1 < n && (p[i + 1] == '@' || p[i + 1] == '[' || p[i + 1] == '{')) return false;
     }
     // parseObjectPath repeatedly on the remainder
     size_t pos = 0;
+    bool list_seen = false;
     for (;;) {
         PathComponent comp;
         std::string part;
@@ -84,8 +85,13 @@ bool split_selector(const std::string& p, std::vector<PathComponent>* out) {
         size_t dot = p.find('.', pos);
         std::string raw = p.substr(pos, (dot == std::string::npos ? n : dot) - pos);
         comp.key = part;
-        comp.array_index = raw == "#" ? kArrCount
+        comp.array_index = raw == "#" ? (more ? kArrList : kArrCount)
                            : escaped && raw.find('\\') != std::string::npos ? -1 : array_index_of(raw);
+        // "#." lists: the key path after the list part holds no '#' (gjson would run a
+        // nested '#' form per element); other parts with a '#' never match an element
+        // (parseArrayPath's arrch without a count or a list)
+        if (list_seen && raw.find('#') != std::string::npos) return false;
+        if (comp.array_index == kArrList) list_seen = true;
         out->push_back(comp);
         if (!more) break;
         pos = next;
@@ -546,7 +552,8 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             std::vector<ModSpec> mspec;
             const int mr = split_modifiers(sel, &base, &mspec);
             const bool ok_path = mr >= 0 && split_selector(base, &pc);
-            const bool counted = ok_path && !pc.empty() && pc.back().array_index == kArrCount;
+            bool counted = false;  // a '#' count or list: the exact scan (no modifier chain after it)
+            for (const PathComponent& c : pc) counted = counted || c.array_index == kArrCount || c.array_index == kArrList;
             if (!ok_path || (counted && !mspec.empty()) || comps.size() + pc.size() > 0xFFFFu ||
                 mods.size() + mspec.size() > 0xFFFFu) {
                 p.state = P_UNSUPPORTED;
@@ -601,7 +608,10 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     // (modifier chains run in the exact scan only: such a ruleset has no single-pass tables)
     // (a count selector is answered by the exact scan only)
     bool fast_ok = np <= kFastMaxPatterns && sels.size() <= kFastMaxSelectors && mods.empty();
-    for (const Component& c : comps) fast_ok = fast_ok && c.array_index != kArrCount;
+    for (const Component& c : comps) {
+        fast_ok = fast_ok && c.array_index != kArrCount && c.array_index != kArrList;
+        if (c.array_index == kArrList) flags |= kFlagBufs;
+    }
     for (size_t s = 0; s < sels.size() && fast_ok; s++) {
         uint32_t cur = 0;
         for (uint32_t k = 0; k < sels[s].comp_count; k++) {

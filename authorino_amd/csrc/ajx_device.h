@@ -42,6 +42,9 @@ struct ValueRef {
 // ValueRef::esc of a Number that is an array's element count (a "#" part, kArrCount):
 // not a document span — the count is in `start` (start == end)
 constexpr uint8_t kValCount = 2;
+// ValueRef::esc of the array a "#." list part stopped at (kArrList): [start, end) is the
+// array; the exact scan builds the list text from it (ajx_modifiers.h build_list)
+constexpr uint8_t kValList = 3;
 
 // ---------------------------------------------------------------------------------
 // scanning primitives (gjson parseString / parseSquash / parseNumber / parseLiteral)
@@ -540,9 +543,11 @@ AJX_HD ValueRef gj_get(const uint8_t* d, uint32_t n, const Component* comps, uin
     if (i >= n || nc == 0) return none;
     uint8_t ftype[kMaxComponents];
     int32_t fh[kMaxComponents];
+    uint32_t fs[kMaxComponents];  // the container's opening bracket
     int depth = 0;
     ftype[0] = d[i];
     fh[0] = 0;
+    fs[0] = i;
     i++;
     for (;;) {
         const Component& c = comps[depth];
@@ -603,6 +608,7 @@ AJX_HD ValueRef gj_get(const uint8_t* d, uint32_t n, const Component* comps, uin
                     depth++;
                     ftype[depth] = ch;
                     fh[depth] = 0;
+                    fs[depth] = i;
                     i++;
                     pushed = true;
                     break;
@@ -637,6 +643,14 @@ AJX_HD ValueRef gj_get(const uint8_t* d, uint32_t n, const Component* comps, uin
                     v.start = v.end = (uint32_t)(fh[depth] - 1);
                     v.type = T_NUMBER;
                     v.esc = kValCount;
+                    return v;
+                }
+                if (c.array_index == kArrList) {  // parseArray alog: the list is built at ']'
+                    ValueRef v;
+                    v.start = fs[depth];
+                    v.end = i + 1;
+                    v.type = T_JSON;
+                    v.esc = kValList;
                     return v;
                 }
                 i++;

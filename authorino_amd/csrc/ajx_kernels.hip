@@ -77,6 +77,13 @@ __device__ __forceinline__ void eval_scan_one(uint32_t r, const uint8_t* const* 
         if (pt.state != P_OK) return eval_pattern<true>(blob, pt, doc, ValueRef{0, 0, T_NULL, 0});
         if constexpr (MODS) {
             const Selector& sl = sels[pt.selector];
+            const ValueRef v = value_of(p);
+            if (v.esc == kValList) {  // a "#." list (no modifier chain after it)
+                const uint8_t* rd;
+                ValueRef rv;
+                if (!build_list(blob, sl, doc, v, *mb, &rd, &rv)) return V_U;
+                return eval_pattern<true>(blob, pt, rd, rv);
+            }
             if (sl.mod_count) {
                 const uint8_t* rd;
                 ValueRef rv;
@@ -770,7 +777,8 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
         const ValueRef v = gj_get(doc, len, comps + sl.comp_begin, sl.comp_count, lits);
         o[0] = v.start;
         o[1] = v.end - v.start;
-        o[2] = (uint32_t)v.type | ((uint32_t)v.esc << 8);
+        // (a "#." list is a built text, not a document span: not selectable)
+        o[2] = v.esc == kValList ? 255u : (uint32_t)v.type | ((uint32_t)v.esc << 8);
     }
 }
 

@@ -262,6 +262,41 @@ AJX_HD void wrap_escaped(const uint8_t* s, uint32_t n, OutBuf& o) {
     o.put('"');
 }
 
+// gjson's "#." list (parseArray with alogok, at the array's ']'): for every element of
+// the array v (kValList), Get(element, the selector's parts after the list part); the raw
+// texts of those that exist, comma-joined in '[' ']', parsed as the Result (*rdoc, *rv).
+// False when the text exceeds the buffer (undecided).
+AJX_HD bool build_list(const uint8_t* blob, const Selector& sel, const uint8_t* doc, const ValueRef& v, ModBufs& mb,
+                       const uint8_t** rdoc, ValueRef* rv) {
+    const RulesetHdr* h = (const RulesetHdr*)blob;
+    const Component* comps = (const Component*)(blob + h->off_components) + sel.comp_begin;
+    const uint8_t* lits = blob + h->off_literals;
+    uint32_t k = 0;
+    while (k < sel.comp_count && comps[k].array_index != kArrList) k++;
+    OutBuf o{mb.a, 0, kModBuf, true};
+    o.put('[');
+    ArrIter it;
+    ValueRef arr = v;
+    arr.esc = 0;
+    it.init(doc, arr);
+    ValueRef e;
+    uint32_t cnt = 0;
+    while (it.next(&e)) {
+        const ValueRef sub = gj_get(doc + e.start, e.end - e.start, comps + k + 1, sel.comp_count - k - 1, lits);
+        if (sub.end <= sub.start) continue;  // (not found; a synthetic value needs no list here)
+        if (cnt++) o.put(',');
+        o.put(doc + e.start + sub.start, sub.end - sub.start);
+    }
+    o.put(']');
+    if (!o.ok) return false;
+    *rdoc = mb.a;
+    rv->start = 0;
+    rv->end = o.n;
+    rv->type = T_JSON;
+    rv->esc = 0;
+    return true;
+}
+
 // Run the selector's modifier chain on the value v of document doc: the final gjson
 // Result as (*rdoc, *rv). Returns false when undecided. A value that does not exist stays
 // Null (gjson pipes into the modifiers only from a found value).

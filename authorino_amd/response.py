@@ -509,7 +509,9 @@ class ValueSelectors:
         if self.paths:
             pats = [(p, int(jsonexp.EqualOperator), "") for p in self.paths]
             self.ruleset = ctx.compile(pats, [], -1)
-            bad = [p for p, st in zip(self.paths, self.ruleset.status) if st != 0]
+            # (a "#." list is a built JSON text, not a document span: not selectable)
+            bad = [p for p, st in zip(self.paths, self.ruleset.status)
+                   if st != 0 or re.search(r"(^|(?<!\\)\.)#\.", p)]
             if bad:
                 from .runtime import AuthjxError
 

@@ -345,6 +345,9 @@ typedef struct {
     const char* path;
     size_t path_len;
     int more, piped, arrch;
+    int alogok;            /* "#.key": the list of each element's key */
+    const char* alogkey;
+    size_t alogkey_len;
 } arrpath;
 
 static void parse_array_path(const char* path, size_t n, arrpath* r) {
@@ -365,7 +368,14 @@ static void parse_array_path(const char* path, size_t n, arrpath* r) {
             }
             return;
         }
-        if (path[i] == '#') r->arrch = 1; /* ("#." and "#(" "#[" forms are rejected up front) */
+        if (path[i] == '#') {
+            r->arrch = 1; /* ("#(" "#[" queries are rejected up front) */
+            if (i == 0 && n > 1 && path[1] == '.') {
+                r->alogok = 1;
+                r->alogkey = path + 2;
+                r->alogkey_len = n - 2;
+            }
+        }
     }
     r->part = path;
     r->part_len = n;
@@ -385,6 +395,30 @@ static int parse_uint(const char* s, size_t n, uint64_t* v) {
 
 static size_t parse_object(pctx* c, size_t i, const char* path, size_t plen, int* hit_out);
 
+/* parseAny (hit): the extent [*s, *e) of the first value at or after json[i] */
+static int any_span(const char* json, size_t len, size_t i, size_t* s, size_t* e) {
+    for (; i < len; i++) {
+        unsigned char ch = (unsigned char)json[i];
+        if (ch <= ' ') continue;
+        *s = i;
+        if (ch == '"') {
+            size_t rs, re; int esc, ok;
+            size_t k = parse_string(json, len, i + 1, &rs, &re, &esc, &ok);
+            *e = k;
+            return ok;
+        }
+        if (ch == '{' || ch == '[') { parse_squash(json, len, i, e); return 1; }
+        if (ch == 'n' && !(i + 1 < len && json[i + 1] != 'u')) { *e = parse_literal(json, len, i); return 1; }
+        if (ch == 't' || ch == 'f') { *e = parse_literal(json, len, i); return 1; }
+        if (ch == '-' || ch == '+' || (ch >= '0' && ch <= '9') || ch == 'i' || ch == 'I' || ch == 'N' || ch == 'n') {
+            *e = parse_number(json, len, i);
+            return 1;
+        }
+        /* (anything else, e.g. the ',' an element position starts at: skipped) */
+    }
+    return 0;
+}
+
 static size_t parse_array(pctx* c, size_t i, const char* path, size_t plen, int* hit_out) {
     arrpath rp;
     parse_array_path(path, plen, &rp);
@@ -394,10 +428,13 @@ static size_t parse_array(pctx* c, size_t i, const char* path, size_t plen, int*
     const char* json = c->json;
     size_t len = c->len;
     int64_t h = 0;
+    size_t alog[4096];
+    size_t nalog = 0;
     while (i < len + 1) {
         int pmatch = (partidx == h);
         int hit = pmatch && !rp.more;
         h++;
+        if (rp.alogok && nalog < sizeof alog / sizeof alog[0]) alog[nalog++] = i;
         for (;; i++) {
             unsigned char ch;
             if (i > len) break;
@@ -453,7 +490,39 @@ static size_t parse_array(pctx* c, size_t i, const char* path, size_t plen, int*
                     num = 1;
                     break;
                 case ']':
-                    if (rp.arrch && rp.part_len == 1 && rp.part[0] == '#') {
+                    if (rp.arrch && rp.part_len == 1 && rp.part[0] == '#' && rp.alogok) {
+                        /* the list: Get(element, alogkey).Raw of each element where it exists */
+                        or_buf lst = {0};
+                        or_buf_push(&lst, "[", 1);
+                        size_t k = 0;
+                        for (size_t j = 0; j < nalog; j++) {
+                            size_t idx = alog[j];
+                            while (idx < len && (json[idx] == ' ' || json[idx] == '\t' || json[idx] == '\r' ||
+                                                 json[idx] == '\n'))
+                                idx++;
+                            size_t es, ee;
+                            if (idx < len && json[idx] != ']' && any_span(json, len, idx, &es, &ee)) {
+                                or_result sub;
+                                memset(&sub, 0, sizeof sub);
+                                if (or_gjson_get(json + es, ee - es, rp.alogkey, rp.alogkey_len, &sub) == 0 &&
+                                    sub.raw_len > 0) {
+                                    if (k++) or_buf_push(&lst, ",", 1);
+                                    or_buf_push(&lst, sub.raw, sub.raw_len);
+                                }
+                                or_result_free(&sub);
+                            }
+                        }
+                        or_buf_push(&lst, "]", 1);
+                        or_buf_reset(&c->value->own);
+                        or_buf_push(&c->value->own, lst.p, lst.n);
+                        or_buf_free(&lst);
+                        c->value->type = OR_JSON;
+                        c->value->raw = c->value->own.p;
+                        c->value->raw_len = c->value->own.n;
+                        *hit_out = 1;
+                        return i + 1;
+                    }
+                    if (rp.arrch && rp.part_len == 1 && rp.part[0] == '#' && !rp.more) {
                         /* the element count: Number(h - 1), Raw = strconv.Itoa(h - 1) */
                         char dg[24];
                         int nd = snprintf(dg, sizeof dg, "%lld", (long long)(h - 1));
@@ -590,9 +659,13 @@ int or_path_supported(const char* p, size_t n) {
         char c = p[i];
         if (c == '\\') { i++; if (i < n && (p[i] == '|' || p[i] == '#')) return -1; continue; }
         if (c == '|' || c == '*' || c == '?') return -1;
-        /* '#' array forms: "#.key" lists and "#(" "#[" queries are not restated; a
-         * part "#" on an array is its element count */
-        if (c == '#' && i + 1 < n && (p[i + 1] == '.' || p[i + 1] == '(' || p[i + 1] == '[')) return -1;
+        /* '#' array forms: "#(" "#[" queries are not restated; a part "#" on an array
+         * is its element count, "#.key" the list of the elements' keys (no further '#'
+         * in that key path) */
+        if (c == '#' && i + 1 < n && (p[i + 1] == '(' || p[i + 1] == '[')) return -1;
+        if (c == '#' && i + 1 < n && p[i + 1] == '.' && (i == 0 || p[i - 1] == '.') &&
+            memchr(p + i + 1, '#', n - i - 1))
+            return -1;
         if (c == '.' && i + 1 < n && (p[i + 1] == '@' || p[i + 1] == '[' || p[i + 1] == '{')) return -1;
     }
     return 0;

@@ -53,6 +53,15 @@ int ht_eval(void* h, const uint8_t* doc_in, uint32_t len, uint8_t* res, int32_t*
             const Selector& s = sels[pats[p].selector];
             v = gj_get(doc, len, comps + s.comp_begin, s.comp_count, lits);
         }
+        if (pats[p].state == P_OK && v.esc == kValList) {  // a "#." list (the kernel's build_list)
+            static ModBufs mb;
+            const uint8_t* rd;
+            ValueRef rv;
+            res[p] = build_list(blob, sels[pats[p].selector], doc, v, mb, &rd, &rv)
+                         ? eval_pattern<true>(blob, pats[p], rd, rv)
+                         : (uint8_t)V_U;
+            continue;
+        }
         if (pats[p].state == P_OK && sels[pats[p].selector].mod_count) {
             static ModBufs mb;  // (the kernel's work-item scratch)
             const uint8_t* rd;
@@ -102,6 +111,23 @@ int ht_string(const char* path, uint32_t plen, const uint8_t* doc_in, uint32_t l
         comps.push_back(k);
     }
     ValueRef v = gj_get(doc, len, comps.data(), (uint32_t)comps.size(), (const uint8_t*)lits.data());
+    static ModBufs mb;
+    if (v.esc == kValList) {  // a "#." list: its text from build_list
+        std::vector<uint8_t> blob(sizeof(RulesetHdr) + comps.size() * sizeof(Component) + lits.size() + 16, 0);
+        RulesetHdr* hd = (RulesetHdr*)blob.data();
+        hd->off_components = sizeof(RulesetHdr);
+        hd->off_literals = (uint32_t)(sizeof(RulesetHdr) + comps.size() * sizeof(Component));
+        std::memcpy(blob.data() + hd->off_components, comps.data(), comps.size() * sizeof(Component));
+        std::memcpy(blob.data() + hd->off_literals, lits.data(), lits.size());
+        Selector sel{0, (uint16_t)comps.size(), 0, 0};
+        const uint8_t* rd;
+        ValueRef rv;
+        if (!build_list(blob.data(), sel, doc, v, mb, &rd, &rv)) return -1;
+        uint32_t k = 0;
+        for (uint32_t i = rv.start; i < rv.end; i++)
+            if (k < cap) out[k++] = rd[i];
+        return (int)k;
+    }
     StrSrc s;
     if (!string_of<true>(doc, v, &s)) return -1;
     uint32_t k = 0;

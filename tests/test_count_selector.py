@@ -1,7 +1,8 @@
-"""gjson `#` (array element count) selectors: `groups.#`, `a.0.#`, `#` on a root array —
-gjson v1.14.0 parseArray answers Number(element count) at the array's ']' (Raw =
-strconv.Itoa); on an object the part is the key "#". `#.key` lists and `#(...)` queries
-stay AUTHJX_PAT_UNSUPPORTED. No reference test covers `#` (parity unpinned: the cases
+"""gjson `#` selectors: `groups.#` / `a.0.#` / `#` (array element count — gjson v1.14.0
+parseArray answers Number(count) at the array's ']', Raw = strconv.Itoa) and `friends.#.first`
+lists (parseArray's alog: the JSON array of Get(element, "first").Raw over the elements
+where it exists); on an object the part is the key "#". `#(...)` / `#[...]` queries and
+a '#' form inside a list's key path stay AUTHJX_PAT_UNSUPPORTED. No reference test covers `#` (parity unpinned: the cases
 below follow gjson's documented semantics, e.g. its README's `friends.#` -> 3); the
 device exact scan (host build, tests/native) is checked against the oracle
 restatement (oracle/gjson_ref.c), and tests/test_gpu_parity.py checks the GPU."""
@@ -22,6 +23,14 @@ KATS = [  # (document, path, Result.String(), found)
     ('{"a":"x"}', "a.#", b"", False),
     ('{"a":[1,2]}', "b.#", b"", False),
     ('{"a" : [ 1 , 2 ] }', "a.#", b"2", True),
+    ('{"friends":[{"first":"Dale"},{"first":"Roger"},{"last":"x"},3,"s",{"first":{"a":1}}]}', "friends.#.first",
+     b'["Dale","Roger",{"a":1}]', True),
+    ('{"a":[]}', "a.#.b", b"[]", True),
+    ('{"a":{"#":{"b":7}}}', "a.#.b", b"7", True),  # object context: key "#", then b
+    ('{"a":[{"b":{"c":1}},{"b":{"c":2}}]}', "a.#.b.c", b"[1,2]", True),
+    ('{"a":[ {"b":"x\\"y"} , {"b":null} ]}', "a.#.b", b'["x\\"y",null]', True),
+    ('[{"x":1},{"x":2}]', "#.x", b"[1,2]", True),
+    ('{"a":"s"}', "a.#.b", b"", False),
 ]
 
 
@@ -32,8 +41,8 @@ def test_count_kats_oracle_and_exact_scan(doc, path, want, found):
     assert H.string(doc, path) == want
 
 
-def test_count_queries_and_lists_unsupported():
-    for path in ["a.#.b", "a.#(b==1)", "a.#[b==1]", "#.x"]:
+def test_count_queries_and_nested_lists_unsupported():
+    for path in ["a.#(b==1)", "a.#[b==1]", "a.#.b.#", "a.#.#.c"]:
         with pytest.raises(ValueError):
             O.gjson_get(b'{"a":[]}', path.encode())
         hr = H.HostRuleset([(path, 1, "1")], [(0, -1, -1, 0)], 0)
@@ -44,10 +53,16 @@ def rand_count_patterns(rng, k):
     pats = []
     for _ in range(k):
         sel = FU.rand_selector(rng)
-        if rng.random() < 0.6:
+        r = rng.random()
+        if r < 0.4:
             sel = "#" if rng.random() < 0.1 else sel + ".#"
+        elif r < 0.7:  # a list: the key path after it from the random keys
+            sel = sel + ".#." + FU.rand_selector(rng)
         op = int(rng.choice([1, 2, 3, 4, 5]))
-        val = str(int(rng.integers(0, 6))) if op != 5 else ["^[0-9]$", "^0$", "[2-4]"][int(rng.integers(0, 3))]
+        val = (str(int(rng.integers(0, 6))) if rng.random() < 0.6 else
+               ["[]", '["x"]', "v3", "[1]", "true", '["hello"]'][int(rng.integers(0, 6))])
+        if op == 5:
+            val = ["^[0-9]$", "^0$", "[2-4]", "^\\[\\]$", "v"][int(rng.integers(0, 5))]
         pats.append((sel, op, val))
     return pats
 
