@@ -330,11 +330,17 @@ struct Scan {
         if (parent == kNoNode) return;
         // (a live node always has children: open_container stores only those)
         str_open = open_before(i);
+#ifndef AJX_ABLATE_KEY_NOESC  // (profiling variants of the key lookup; outputs may differ)
         const uint32_t lb = last_bs_before(i);
         if (lb != ~0u && lb > str_open) { st = X_SLOW; return; }  // escaped key on a live path
+#endif
         const uint32_t k0 = str_open + 1, klen = p - k0;
+#ifdef AJX_ABLATE_KEY_NOSIG
+        uint64_t sig = klen;
+#else
         uint64_t sig = tail8(i);
         if (klen < 8) sig = klen ? sig >> (8 * (8 - klen)) : 0ull;
+#endif
         const uint32_t want = (klen & 0xFFFFu) | (parent << 16), mask = (1u << ks_log2) - 1u;
         uint32_t at = key_slot_hash(sig, klen, parent, ks_log2);
         for (uint32_t probe = 0; probe <= mask; probe++, at = (at + 1) & mask) {
@@ -344,17 +350,26 @@ struct Scan {
             bool eq = true;
             const uint8_t* kl = lits + slot.key_off;
             const uint32_t a0 = k0 + (wa - (uint32_t)bpos);  // ring position of the key's first byte
+#ifdef AJX_ABLATE_KEY_NOCMP
+            if (false) {
+#else
             if (a0 + 64u >= wa) {  // the key began in the ring's windows: compare from LDS
+#endif
                 for (uint32_t k = 0; k + 8 < klen; k += 4) {
                     const uint32_t r = klen - 8 - k;
                     const uint32_t m = r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
                     if ((ring.u32(a0 + k) ^ load_u32_any(kl + k)) & m) { eq = false; break; }
                 }
             } else {
+#ifndef AJX_ABLATE_KEY_NOCMP
                 for (uint32_t k = 0; k + 8 < klen; k++)
                     if (d[k0 + k] != kl[k]) { eq = false; break; }
+#endif
             }
             if (eq) { pending = slot.meta >> 24; return; }
+#ifdef AJX_ABLATE_KEY_PROBE1
+            return;
+#endif
         }
     }
 

@@ -3,9 +3,9 @@
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1; shift
-mkdir -p scripts/bin
+mkdir -p scripts/bin scripts/var
 B=authorino_amd/csrc/build
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-function "$@" -c authorino_amd/csrc/ajx_kernels.hip -o scripts/bin/k_$NAME.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o scripts/bin/libauthjx_$NAME.so $B/ajx_regex.cpp.o $B/ajx_compiler.cpp.o $B/ajx_api.cpp.o scripts/bin/k_$NAME.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o scripts/var/libauthjx_$NAME.so $B/*.cpp.o scripts/bin/k_$NAME.o
 rm -f scripts/bin/k_$NAME.o
-echo scripts/bin/libauthjx_$NAME.so
+echo scripts/var/libauthjx_$NAME.so

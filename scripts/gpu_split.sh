@@ -1,7 +1,6 @@
-# per-kernel split of the fast path (mode 3: stage A and stage B as two launches) on c2
-set -u
-R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out
-mkdir -p $O
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_split -o run -- python3 $R/scripts/ablate_scan.py c2 > $O/prof_split.log 2>&1 || exit $?
+# stage A / stage B split (mode 3: two launches) against the single-pass kernel
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/split && export TMPDIR=/tmp
+for w in c2 c3; do
+  timeout -k 10 200 python scripts/ablate_scan.py $w 1048576 0,3 > gpurun_out/split/ab_$w.log 2>&1 || exit $?
+done
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/split/st_c3 -o c3 -- python3 $GRAFT_REPO_ROOT/scripts/ablate_scan.py c3 1048576 3 > $GRAFT_REPO_ROOT/gpurun_out/split/st_c3.log 2>&1 || exit $?

@@ -448,20 +448,29 @@ def test_select_from_eval_matches_select_batch(ctx):
         ctx.select_from_eval_device(fused, fused.n_patterns - k, A, Of, Ln, got)
 
 
-def test_lane_kernel_matches_oracle(ctx):
-    """The lane kernel (kernel mode 20, ajx_lane.h) on the c2 / c3 workloads, random and
-    malformed documents: the same outputs as the oracle."""
+@pytest.mark.parametrize("mode", [20, 31])
+def test_alternative_stage_a_matches_oracle(ctx, mode):
+    """The lane kernel (kernel mode 20, ajx_lane.h) and the event scanner (mode 31,
+    ajx_events.h) on the c2 / c3 workloads, random and malformed documents (and c4's
+    multi-tenant kernel for the event scanner): the same outputs as the oracle."""
     import fuzz_util as FU
     from authorino_amd import workloads as W
 
-    ctx.set_kernel_mode(20)
+    ctx.set_kernel_mode(mode)
     try:
         for workload, n in (("c2", 50000), ("c3", 20000)):
             w = W.make(workload, n=n, seed=31)
             rs = ctx.compile_expression(w.expr)
             tri, err, bm = ctx.eval_host_arena([rs], w.arena, w.offs, w.lens)
-            assert ctx.last_exact_count() == 0  # every synthetic document took the lane path
+            assert ctx.last_exact_count() == 0  # every synthetic document stayed on the fast path
             otri, oerr, obm = _oracle(w.expr, w.arena, w.offs, w.lens)
+            assert np.array_equal(tri, otri) and np.array_equal(err, oerr) and np.array_equal(bm, obm)
+        if mode == 31:
+            w = W.make("c4", n=30000, seed=32)
+            rss = [ctx.compile_expression(e) for e in w.exprs]
+            tri, err, bm = ctx.eval_host_arena(rss, w.arena, w.offs, w.lens, set_of_req=w.set_of_req)
+            osets = [O.Ruleset.from_expression(e) for e in w.exprs]
+            otri, oerr, obm = _oracle(None, w.arena, w.offs, w.lens, set_of_req=w.set_of_req, sets=osets)
             assert np.array_equal(tri, otri) and np.array_equal(err, oerr) and np.array_equal(bm, obm)
         rng = np.random.default_rng(78)
         for _ in range(20):
