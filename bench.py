@@ -48,6 +48,8 @@ def parse():
                     help="CPU/gloo test of the distributed driver: no GPU, a stand-in step")
     ap.add_argument("--kernel-mode", type=int, default=0,
                     help="0 the single-pass kernel (default), 20 the lane kernel; others: profiling ablations")
+    ap.add_argument("--gather-decisions", action="store_true",
+                    help="N>1: all-gather every rank's decision bitmap inside each step (SURVEY.md §8e, optional)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -148,6 +150,41 @@ def phase_cpu_baseline(w, exprs, target_s, gpu_tri):
                                       f"{threads} host threads, {dt:.1f}s"}, {"sample": k, "mismatches": mism}
 
 
+def decision_bitmap(torch, tri, T, weights):
+    """One bit per (request, tree) result that is T, LSB first (entry k at bit k % 8 of byte
+    k // 8): the decision bitmap a front-end reads. tri: u8 results, length a multiple of 8."""
+    return ((tri == T).view(-1, 8).to(torch.uint8) * weights).sum(dim=1, dtype=torch.uint8)
+
+
+class DecisionGather:
+    """The optional exchange of SURVEY.md §8e: every rank's decision bitmap all-gathered
+    into one (world × bytes) buffer on every rank, with one all_gather_into_tensor (RCCL
+    over xGMI on the GPU, gloo in the CPU tests) per step. Off by default: the shards are
+    independent and the bench value needs no collective."""
+
+    def __init__(self, torch, dist, world, rank, n_entries, T, dev):
+        if n_entries % 8:
+            raise ValueError("decision gather: results per rank must be a multiple of 8")
+        self.torch, self.dist, self.world, self.rank, self.T = torch, dist, world, rank, T
+        self.weights = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=dev)
+        self.out = torch.empty(world * (n_entries // 8), dtype=torch.uint8, device=dev)
+        self.popcount = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.int64, device=dev)
+
+    def __call__(self, tri):
+        self.local = decision_bitmap(self.torch, tri, self.T, self.weights)
+        self.dist.all_gather_into_tensor(self.out, self.local)
+
+    def report(self, dev=None) -> dict:
+        """Checks every rank's slice of the gathered buffer against that rank's own bitmap
+        (a MIN over ranks of the per-rank check)."""
+        nb = self.local.numel()
+        ok = bool(self.torch.equal(self.out[self.rank * nb:(self.rank + 1) * nb], self.local))
+        t = self.torch.tensor([1 if ok else 0], dtype=self.torch.int32, device=self.out.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        return {"ranks": self.world, "bytes_per_rank": nb, "bytes_gathered": int(self.out.numel()),
+                "allowed_bits": int(self.popcount[self.out.long()].sum()), "slices_equal_to_local": bool(int(t[0]))}
+
+
 def timed_steps(step, steps, warmup, dist, torch, dev, stream=None):
     """W untimed steps, then exactly K timed steps bracketed by barrier + synchronize on
     both sides; returns (wall seconds, mean per-step event ms on `stream`), each the max
@@ -207,6 +244,12 @@ def c1_cpu_ns_per_op(reps: int = 200000) -> dict:
                     "the published Go figure is 1.797 us/op for 2 eq patterns on a Xeon 8370C core"}
 
 
+def parallelism(world, gather) -> str:
+    if gather:
+        return f"dp{world} (independent request shards; all-gather of decision bitmaps per step)"
+    return f"dp{world} (independent request shards, no collective)"
+
+
 def dry_main(args, world, rank, dist, torch) -> None:
     """The distributed driver without a GPU (gloo): same sharding, seeds, barriers, timing
     and JSON line; the step is a stand-in (a checksum over the rank's shard)."""
@@ -215,11 +258,19 @@ def dry_main(args, world, rank, dist, torch) -> None:
     seed = workloads.DEFAULT_SEEDS.get(args.workload, 0) + 7919 * rank
     w = workloads.make(args.workload, n=args.n or 256, seed=seed, unique=args.unique or 64, uniquify=True)
     acc = [0]
+    gather = None
+    if args.gather_decisions and dist:
+        # stand-in results: one byte per request from its length (T = 1)
+        tri = torch.from_numpy((w.lens % 3).astype(np.uint8))
+        gather = DecisionGather(torch, dist, world, rank, tri.numel(), 1, "cpu")
 
     def step():
         acc[0] += int(w.arena.sum(dtype=np.uint64)) + int(w.lens.sum())
+        if gather:
+            gather(tri)
 
     elapsed, _ = timed_steps(step, args.steps, args.warmup, dist, torch, None)
+    gathered = gather.report() if gather else None
     shard = {"rank": rank, "seed": seed, "n": w.n, "first_doc_sha": __import__("hashlib").sha1(w.doc(0)).hexdigest()}
     shards = [None] * world
     if dist:
@@ -231,9 +282,9 @@ def dry_main(args, world, rank, dist, torch) -> None:
                           "unit": "request×rule evals/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
                           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-                          "data": "synthetic", "dry_run": True, "shards": shards,
+                          "data": "synthetic", "dry_run": True, "shards": shards, "decision_gather": gathered,
                           "config": {"workload": args.workload, "requests_per_gpu": w.n,
-                                     "parallelism": f"dp{world} (independent request shards, no collective)"}}),
+                                     "parallelism": parallelism(world, gather)}}),
               flush=True)
 
 
@@ -309,12 +360,20 @@ def main():
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
+    gather = DecisionGather(torch, dist, world, rank, tri.numel(), runtime.T, dev) \
+        if args.gather_decisions and dist else None
+
     def step():
         ctx.eval_device(rss, arena, offs, lens, tri, err, bm, set_of_req=sor, stream=sp)
         if phase:
             ctx.select_from_eval_device(rss[0], r_phase, arena, offs, lens, spans, stream=sp)
+        if gather:
+            gather(tri)  # (on `stream`, the current stream: inside the timed step)
 
+    extra = {}
     elapsed, kern_ms = timed_steps(step, args.steps, args.warmup, dist, torch, dev, stream)
+    if gather:
+        extra["decision_gather"] = gather.report()
 
     total_req = w.n * args.steps * world
     value = int(rpr.sum()) * args.steps * world / elapsed  # shards are equal-sized (weak scaling)
@@ -336,7 +395,6 @@ def main():
         pass
 
     cpu, parity, c1, pcie = None, None, None, None
-    extra = {}
     tri_h = tri.cpu().numpy()
     if phase:
         # the phase decision from the per-tree results (auth_pipeline.go:454-457, :287-322)
@@ -410,7 +468,7 @@ def main():
                 "auth_configs": len(rss),
                 "trees_per_request": nt_out,
                 "doc_bytes_mean": float(w.lens.mean()),
-                "parallelism": f"dp{world} (independent request shards, no collective)",
+                "parallelism": parallelism(world, gather),
             },
             "roofline": {
                 "bound": "hbm",
@@ -420,6 +478,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
                 "kernel_ms": kern_ms,
+                **({"note": "kernel_ms is the whole step's event time, decision all-gather included"}
+                   if gather else {}),
                 "algorithmic_bytes_per_launch": algo_bytes,
             },
             "cpu_baseline": cpu,

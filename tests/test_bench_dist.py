@@ -74,3 +74,57 @@ def test_bench_gpus2_relaunches_two_ranks():
     assert shards[0]["seed"] != shards[1]["seed"]
     assert shards[0]["first_doc_sha"] != shards[1]["first_doc_sha"]  # independent shards
     assert all(s["n"] == 96 for s in shards)
+
+
+@pytest.mark.timeout(300)
+def test_bench_gather_decisions_two_ranks():
+    """--gather-decisions (optional): each step all-gathers every rank's
+    decision bitmap; every rank finds its own bitmap in its slice of the gathered buffer."""
+    import subprocess
+
+    import numpy as np
+
+    sys.path.insert(0, ROOT)
+    from authorino_amd import workloads
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--gather-decisions", "--workload", "c2", "--n", "96", "--steps", "2", "--warmup", "1"],
+                         capture_output=True, text=True, env=env, timeout=280, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    g = rec["decision_gather"]
+    assert g["ranks"] == 2 and g["bytes_per_rank"] == 12 and g["bytes_gathered"] == 24
+    assert g["slices_equal_to_local"]
+    # the stand-in results are lens % 3 (T = 1) on each rank's own shard
+    want = 0
+    for r in range(2):
+        w = workloads.make("c2", n=96, seed=workloads.DEFAULT_SEEDS["c2"] + 7919 * r, unique=64, uniquify=True)
+        want += int((w.lens % 3 == 1).sum())
+    assert g["allowed_bits"] == want
+    assert "all-gather" in rec["config"]["parallelism"]
+
+
+def test_decision_bitmap_layout():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    tri = torch.tensor([1, 0, 1, 1, 2, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1], dtype=torch.uint8)
+    wts = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8)
+    got = bench.decision_bitmap(torch, tri, 1, wts)
+    assert got.tolist() == [0b00101101, 0b10000000]
+
+
+@pytest.mark.gpu
+def test_decision_bitmap_on_device():
+    """The bitmap bench.py all-gathers, built by the same torch ops on the GPU."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    g = torch.Generator().manual_seed(5)
+    tri = torch.randint(0, 4, (4096,), generator=g, dtype=torch.uint8)
+    wts = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8)
+    want = bench.decision_bitmap(torch, tri, 1, wts)
+    got = bench.decision_bitmap(torch, tri.cuda(), 1, wts.cuda()).cpu()
+    assert torch.equal(got, want)
+    assert int(want[0]) == sum(1 << k for k in range(8) if int(tri[k]) == 1)
