@@ -52,6 +52,8 @@ struct Workspace {
     // rows_rs over rows_n requests on this stream (nullptr: none usable)
     const authjx_ruleset* rows_rs = nullptr;
     uint32_t rows_n = 0, rows_stride = 0;
+    const uint32_t* rows_perm = nullptr;  // that evaluation's work-item order (d_perm or none)
+    bool rows_wave = false;               // rows in the fused kernels' wave-interleaved layout
     bool ran = false;  // ev0 / ev1 recorded
 };
 
@@ -160,7 +162,9 @@ int ensure_sets(Workspace* w, int device, const authjx_ruleset* const* sets, uin
 // capture rows, slow list and request order for a batch of n (grown when needed, after
 // this stream's earlier batches are done with the old buffers)
 int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
-    if (n <= w->slow_cap && n <= w->perm_cap && (size_t)n * row_stride <= w->rows_cap) return AUTHJX_OK;
+    // (rows for whole waves: the fused kernels' wave-interleaved layout)
+    const size_t rows_need = (size_t)((n + 63u) & ~63u) * row_stride;
+    if (n <= w->slow_cap && n <= w->perm_cap && rows_need <= w->rows_cap) return AUTHJX_OK;
     HIP_OK(hipStreamSynchronize(w->stream));
     w->rows_rs = nullptr;
     if (n > w->slow_cap) {
@@ -177,12 +181,12 @@ int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
         HIP_OK(hipMalloc(&w->d_perm, ((size_t)n + 4096) * sizeof(uint32_t)));
         w->perm_cap = n;
     }
-    if ((size_t)n * row_stride > w->rows_cap) {
+    if (rows_need > w->rows_cap) {
         if (w->d_rows) (void)hipFree(w->d_rows);
         w->d_rows = nullptr;
         w->rows_cap = 0;
-        HIP_OK(hipMalloc(&w->d_rows, (size_t)n * row_stride * sizeof(uint64_t)));
-        w->rows_cap = (size_t)n * row_stride;
+        HIP_OK(hipMalloc(&w->d_rows, rows_need * sizeof(uint64_t)));
+        w->rows_cap = rows_need;
     }
     return AUTHJX_OK;
 }
@@ -379,6 +383,8 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     w->rows_rs = keep_rows ? sets[0] : nullptr;
     w->rows_n = n;
     w->rows_stride = row_stride;
+    w->rows_perm = nullptr;
+    w->rows_wave = !lane;  // (the lane kernel keeps one row per request)
     size_t max_blob = 0;
     for (uint32_t i = 0; i < n_sets; i++) max_blob = std::max(max_blob, sets[i]->c.blob.size());
     if (force_scan) {
@@ -392,6 +398,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
             HIP_OK(ajx::launch_len_order(d_lens, n, w->d_perm + n, w->d_perm, s));
             perm = w->d_perm;
         }
+        w->rows_perm = perm;
         if (lane) {
             const uint32_t stage_bytes =
                 n_sets == 1 && max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u;
@@ -478,7 +485,8 @@ int authjx_select_from_eval_device(authjx_ctx* ctx, const authjx_ruleset* rs, ui
     int rc = ensure_sets(w, ctx->device, one, 1);
     if (rc != AUTHJX_OK) return rc;
     HIP_OK(ajx::launch_select_rows(w->d_sets, d_arena, d_offs, d_lens, n, reinterpret_cast<uint32_t*>(d_out_values),
-                                   values_stride, w->d_rows, w->rows_stride, first_pattern, s));
+                                   values_stride, w->d_rows, w->rows_stride, first_pattern, w->rows_perm,
+                                   w->rows_wave, s));
     return batch_done(w, one, 1);
 }
 

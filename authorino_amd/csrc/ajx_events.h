@@ -315,7 +315,7 @@ struct EvScan : Scan {
 // Stage A with the event automaton for one request; the same contract as scan_doc
 // (ajx_fast.h): true when `row` holds the request's captures, false for the exact scan.
 template <class LoadBlock>
-AJX_HD bool scan_doc_ev(const uint8_t* blob, const Tables& tab, const uint8_t* d, uint32_t n, uint64_t* row,
+AJX_HD bool scan_doc_ev(const uint8_t* blob, const Tables& tab, const uint8_t* d, uint32_t n, RowRef row,
                         const WinRing& ring, LoadBlock load) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
     EvScan s;

@@ -29,6 +29,23 @@ namespace ajx {
 // 8-byte record per selector: low = start, high = len (24 bits) | type << 24 | esc << 27
 constexpr uint64_t kRowSlow = 1ull << 63;
 
+// A capture row in memory: word j at p[j * es]. es = 1: the row's words are contiguous
+// (rows indexed by request); es = 64: the wave-interleaved layout of the fused kernels,
+// where word j of the 64 work-items of a wave is one 512-B run, so a wave's record
+// stores share cache lines and stage B's row reads are coalesced (wave_row).
+struct RowRef {
+    uint64_t* p;
+    uint32_t es;
+    AJX_HD RowRef() : p(nullptr), es(1) {}
+    AJX_HD RowRef(uint64_t* q, uint32_t e = 1) : p(q), es(e) {}
+    AJX_HD RowRef(const uint64_t* q, uint32_t e = 1) : p(const_cast<uint64_t*>(q)), es(e) {}  // (read-only uses)
+    AJX_HD uint64_t& operator[](uint32_t j) const { return p[(size_t)j * es]; }
+};
+// work-item k's row in the wave-interleaved layout of (1 + n_selectors)-word rows
+AJX_HD RowRef wave_row(uint64_t* rows, uint32_t row_stride, uint32_t k) {
+    return RowRef(rows + (size_t)(k & ~63u) * row_stride + (k & 63u), 64u);
+}
+
 AJX_HD uint32_t eq_bytes(uint32_t w, uint32_t c4) {  // 0x80 in every byte equal to c
     uint32_t t = w ^ c4;
     return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
@@ -115,7 +132,7 @@ struct Scan {
     uint32_t ks_log2;
     const uint8_t* lits;
     const uint8_t* d;
-    uint64_t* row;  // capture row (header + records)
+    RowRef row;     // capture row (header + records)
     uint32_t n;
     WinRing ring;
 
@@ -596,7 +613,7 @@ AJX_HD Tables blob_tables(const uint8_t* blob) {
 // request needs the exact scan).
 // MODE (profiling ablations only): 0 = full scan, 1 = loads only, 2 = loads + classification
 template <int MODE = 0, class LoadBlock>
-AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, uint32_t n, uint64_t* row,
+AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, uint32_t n, RowRef row,
                      const WinRing& ring, LoadBlock load) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
     Scan s;
@@ -866,7 +883,7 @@ AJX_HD bool incl_hits(const uint8_t* doc, const ValueRef& v, const Pattern* pats
 
 // Stage B for one request: patterns on the captured values, bitmap, fold.
 // res(p) values are V_T / V_F / V_E / V_U.
-AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, const uint64_t* row, uint64_t t[2],
+AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef row, uint64_t t[2],
                               uint64_t u[2]) {
     // selector by selector: each captured value is decoded once for all its patterns;
     // when its String() is a byte span or a literal, eq/neq compare a dword at a time,

@@ -20,9 +20,12 @@ hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_
 
 // The values of patterns [p0, p0 + stride) of sets[0] from capture rows an earlier
 // single-pass evaluation of that ruleset wrote (no document scan; slow rows: exact Get).
+// d_perm: that evaluation's work-item order (nullptr: identity); wave_rows: the rows are in
+// the fused kernels' wave-interleaved layout (indexed by work-item), else one per request.
 hipError_t launch_select_rows(const uint8_t* const* d_sets, const uint8_t* d_arena, const uint64_t* d_offs,
                               const uint32_t* d_lens, uint32_t n, uint32_t* d_out, uint32_t stride,
-                              const uint64_t* d_rows, uint32_t row_stride, uint32_t p0, hipStream_t stream);
+                              const uint64_t* d_rows, uint32_t row_stride, uint32_t p0, const uint32_t* d_perm,
+                              bool wave_rows, hipStream_t stream);
 
 }  // namespace ajx
 

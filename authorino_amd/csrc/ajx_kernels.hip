@@ -242,7 +242,7 @@ __device__ __forceinline__ WinRing lane_ring(uint32_t ring_off) {
 // stage A for request r: single-pass scan into its capture row (false: slow list)
 // EV: the event scanner (ajx_events.h); otherwise ajx_fast.h's token scanner (the default)
 template <int MODE, bool EV = false>
-__device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t* d, uint32_t len, uint64_t* row,
+__device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t* d, uint32_t len, RowRef row,
                                              const WinRing& ring) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     if (!(h->flags & kFlagFastOk) || len >= (1u << 24)) {
@@ -285,7 +285,7 @@ __device__ __forceinline__ void fold_outputs(uint32_t r, const uint8_t* blob, co
 // stage B for request r on its capture row: patterns, T bitmap, And/Or fold, outputs.
 // false (nothing written): a value needs the exact scan (a number only ajx_float.h
 // decides), the caller hands the request over
-__device__ __forceinline__ bool finish_request(uint32_t r, const uint8_t* blob, const uint8_t* d, const uint64_t* row,
+__device__ __forceinline__ bool finish_request(uint32_t r, const uint8_t* blob, const uint8_t* d, RowRef row,
                                                uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
                                                uint64_t* __restrict__ out_bm, uint32_t stride) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
@@ -355,17 +355,22 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
                                                       int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
                                                       uint32_t stride, uint32_t ring_off,
                                                       const uint32_t* __restrict__ perm) {
-    // work-item k takes request perm[k] (length-bucketed order, see ajx_len_scatter) or k
+    // work-item k takes request perm[k] (length-bucketed order, see ajx_len_scatter) or k;
+    // its capture row is row k of the wave-interleaved layout (wave_row)
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t r = k < n ? (perm ? perm[k] : k) : 0u;
     const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : set_of_req[r]]);
     if (k >= n) return;
-    uint64_t* row = rows + (size_t)r * row_stride;
+    const RowRef row = wave_row(rows, row_stride, k);
     const uint8_t* d = arena + offs[r];
     if (!scan_request<0, EV>(blob, d, lens[r], row, lane_ring(ring_off))) {
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
+#ifdef AJX_ABLATE_FUSED_NOB  // profiling: stage A alone (outputs meaningless)
+    out_tri[r] = (uint8_t)row[0];
+    return;
+#endif
     if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
         row[0] = kRowSlow;
         slow_ids[atomicAdd(slow_count, 1u)] = r;
@@ -393,7 +398,7 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     // (block-uniform: every thread reaches the barrier in stage_blob or none does)
     const bool uni = __syncthreads_and(sid == sid0) &&
                      reinterpret_cast<const RulesetHdr*>(sets[sid0])->total_bytes <= ring_off;
-    uint64_t* row = rows + (size_t)r * row_stride;
+    const RowRef row = wave_row(rows, row_stride, k);
     const uint8_t* d = arena + offs[r];
     if (uni) {
         const uint8_t* blob = stage_blob<true>(gblob);
@@ -731,12 +736,17 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
                                                          const uint32_t* __restrict__ lens, uint32_t n,
                                                          uint32_t* __restrict__ out, uint32_t stride,
                                                          const uint64_t* __restrict__ rows, uint32_t row_stride,
-                                                         uint32_t p0) {
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
+                                                         uint32_t p0, const uint32_t* __restrict__ perm,
+                                                         uint32_t wave_rows) {
+    // work-item k: request perm[k] (the order the rows were written in) or k; its row is
+    // row k of the wave-interleaved layout (wave_rows: the fused kernels') or row r
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t r = perm ? perm[k] : k;
     // the single-pass scan's capture row when it has one (not on the slow list)
-    const uint64_t* row = rows ? rows + (size_t)r * row_stride : nullptr;
-    const uint64_t found = row ? row[0] : kRowSlow;
+    const RowRef row = !rows ? RowRef() : wave_rows ? wave_row(const_cast<uint64_t*>(rows), row_stride, k)
+                                                    : RowRef(rows + (size_t)r * row_stride);
+    const uint64_t found = rows ? row[0] : kRowSlow;
     const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const Selector* sels = reinterpret_cast<const Selector*>(blob + h->off_selectors);
@@ -819,18 +829,19 @@ hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
     hipLaunchKernelGGL(ajx_select_values, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                       d_lens, n, d_out, stride, d_rows, row_stride, 0u);
+                       d_lens, n, d_out, stride, d_rows, row_stride, 0u, nullptr, 0u);
     return hipGetLastError();
 }
 
 hipError_t launch_select_rows(const uint8_t* const* d_sets, const uint8_t* d_arena, const uint64_t* d_offs,
                               const uint32_t* d_lens, uint32_t n, uint32_t* d_out, uint32_t stride,
-                              const uint64_t* d_rows, uint32_t row_stride, uint32_t p0, hipStream_t stream) {
+                              const uint64_t* d_rows, uint32_t row_stride, uint32_t p0, const uint32_t* d_perm,
+                              bool wave_rows, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
     hipLaunchKernelGGL(ajx_select_values, dim3(grid), dim3(block), 0, stream, d_sets, nullptr, d_arena, d_offs,
-                       d_lens, n, d_out, stride, d_rows, row_stride, p0);
+                       d_lens, n, d_out, stride, d_rows, row_stride, p0, d_perm, wave_rows ? 1u : 0u);
     return hipGetLastError();
 }
 
