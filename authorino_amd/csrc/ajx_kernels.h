@@ -33,8 +33,8 @@ namespace ajx {
 
 // Largest ruleset blob the kernels stage into LDS (a batch over one ruleset).
 constexpr uint32_t kMaxSharedBlobBytes = 48 * 1024;
-// multi-tenant batches: the largest blob a 4-wave workgroup stages in LDS next to its
-// window rings (blob + 4 x 8 KiB rings per group keeps 4 groups = 4 waves/SIMD per CU)
+// multi-tenant batches: the LDS a 4-wave workgroup stages its runs' blobs in, next to its
+// window rings (8 KiB + 4 x 8 KiB rings per group keeps 4 groups = 4 waves/SIMD per CU)
 constexpr uint32_t kMaxTenantStageBytes = 8 * 1024;
 
 // `mods` (every launcher): a ruleset of the batch has modifier chains (RulesetHdr

@@ -378,10 +378,13 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
 }
 
 // The single-pass kernel for multi-tenant batches (one ruleset per request through
-// set_of_req; the caller buckets requests by AuthConfig). A workgroup whose requests all
-// use one ruleset copies that blob into LDS, as the uniform-ruleset kernel does, so its
-// table reads are ds_reads; a workgroup straddling two buckets reads the tables from
-// global memory. Dynamic LDS: [blob copy (up to stage_cap bytes)] [window rings].
+// set_of_req; the caller buckets requests by AuthConfig, so a workgroup's requests form a
+// few runs of one ruleset each). The workgroup finds its runs (a run starts where the
+// ruleset differs from the previous work-item's) and copies the blobs of its first runs
+// into LDS, as many as fit the staging region; a wave whose requests all fall in staged
+// runs reads every table from LDS (each lane from its own run's copy), any other wave
+// reads them from global memory. Dynamic LDS: [staging region (ring_off bytes)] [rings].
+constexpr uint32_t kTenantRuns = 8;  // runs a workgroup may stage
 template <bool EV>
 __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_tenant(
     const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
@@ -389,19 +392,52 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     uint64_t* __restrict__ rows, uint32_t row_stride, uint32_t* __restrict__ slow_count,
     uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
     uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t ring_off, const uint32_t* __restrict__ perm) {
-    const uint32_t k0 = blockIdx.x * blockDim.x;  // (< n: the grid covers n)
-    const uint32_t k = k0 + threadIdx.x;
-    const uint32_t r0 = perm ? perm[k0] : k0;
-    const uint32_t r = k < n ? (perm ? perm[k] : k) : r0;
-    const uint32_t sid0 = set_of_req[r0], sid = set_of_req[r];
-    const uint8_t* gblob = sets[sid];
-    // (block-uniform: every thread reaches the barrier in stage_blob or none does)
-    const bool uni = __syncthreads_and(sid == sid0) &&
-                     reinterpret_cast<const RulesetHdr*>(sets[sid0])->total_bytes <= ring_off;
+    extern __shared__ uint4 s_stage[];
+    __shared__ uint32_t s_wcnt[kFastBlock / 64];
+    __shared__ uint32_t s_rsid[kTenantRuns];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, nw = blockDim.x >> 6;
+    const uint32_t k = blockIdx.x * blockDim.x + t;  // (the grid covers n: n > 0 here)
+    const uint32_t kc = k < n ? k : n - 1u;           // (tail threads: the last request's run)
+    const uint32_t r = perm ? perm[kc] : kc;
+    const uint32_t sid = set_of_req[r];
+    bool start = t == 0;
+    if (!start) {
+        const uint32_t kp = (k - 1u) < n ? k - 1u : n - 1u;
+        start = set_of_req[perm ? perm[kp] : kp] != sid;
+    }
+    // run index of every work-item: starts before it in the workgroup, minus one
+    const uint64_t m = __ballot(start);
+    if (lane == 0) s_wcnt[wv] = (uint32_t)__builtin_popcountll(m);
+    __syncthreads();
+    uint32_t base = 0, nrun = 0;
+    for (uint32_t i = 0; i < nw; i++) {
+        const uint32_t c = s_wcnt[i];
+        base += i < wv ? c : 0u;
+        nrun += c;
+    }
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const uint32_t ridx = base + (uint32_t)__builtin_popcountll(m & upto) - 1u;
+    if (start && ridx < kTenantRuns) s_rsid[ridx] = sid;
+    __syncthreads();
+    // stage the leading runs' blobs while they fit (every thread walks the same list)
+    uint32_t nst = 0, off = 0, my_off = 0;
+    const uint32_t nr = nrun < kTenantRuns ? nrun : kTenantRuns;
+    for (uint32_t j = 0; j < nr; j++) {
+        const uint8_t* g = sets[s_rsid[j]];
+        const uint32_t bytes = reinterpret_cast<const RulesetHdr*>(g)->total_bytes;  // (a multiple of 16)
+        if (off + bytes > ring_off) break;
+        const uint4* src = reinterpret_cast<const uint4*>(g);
+        for (uint32_t i = t; i < bytes / 16u; i += blockDim.x) s_stage[off / 16u + i] = src[i];
+        if (j == ridx) my_off = off;
+        off += bytes;
+        nst++;
+    }
+    __syncthreads();
     const RowRef row = wave_row(rows, row_stride, k);
     const uint8_t* d = arena + offs[r];
-    if (uni) {
-        const uint8_t* blob = stage_blob<true>(gblob);
+    // (wave-uniform: the whole wave takes the LDS tables or the global ones)
+    if (__all(ridx < nst)) {
+        const uint8_t* blob = reinterpret_cast<const uint8_t*>(s_stage) + my_off;
         if (k >= n) return;
         if (!scan_request<0, EV>(blob, d, lens[r], row, lane_ring(ring_off)) ||
             !finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
@@ -409,6 +445,7 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
             slow_ids[atomicAdd(slow_count, 1u)] = r;
         }
     } else {
+        const uint8_t* gblob = sets[sid];
         if (k >= n) return;
         if (!scan_request<0, EV>(gblob, d, lens[r], row, lane_ring(ring_off)) ||
             !finish_request(r, gblob, d, row, out_tri, out_err, out_bm, stride)) {
@@ -945,8 +982,10 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     } else if (d_set_of_req && shared_blob_bytes && shared_blob_bytes <= kMaxTenantStageBytes) {
         // multi-tenant batch: shared_blob_bytes = the largest ruleset blob of the batch;
         // 4-wave workgroups, so more of them fall inside one AuthConfig's bucket
+        // (staging region: the tenant budget less room for the kernel's static LDS, so
+        // four groups still fit a CU)
         const uint32_t tblock = 256, tgrid = (n + tblock - 1) / tblock;
-        const uint32_t toff = (shared_blob_bytes + 15u) & ~15u;
+        const uint32_t toff = kMaxTenantStageBytes - 256u;
         if (ev)
             hipLaunchKernelGGL(ajx_scan_fused_tenant<true>, dim3(tgrid), dim3(tblock),
                                toff + (tblock / 64) * kWinRingBytesPerWave, stream, d_sets, d_set_of_req, d_arena,
