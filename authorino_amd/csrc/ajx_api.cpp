@@ -407,12 +407,11 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
                                          w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s, ablate - 20, perm,
                                          mods));
         } else {
-            // uniform batch: the blob staged once per workgroup; multi-tenant batch: the
-            // largest blob, for workgroups whose requests share one ruleset
-            // (ajx_scan_fused_tenant)
+            // uniform batch: the blob staged once per workgroup; multi-tenant batch: nonzero
+            // turns on the per-workgroup staging of its runs' rulesets (ajx_scan_fused_tenant)
             const uint32_t stage_bytes =
                 n_sets == 1 ? (max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u)
-                            : (!no_tenant_stage && max_blob <= ajx::kMaxTenantStageBytes ? (uint32_t)max_blob : 0u);
+                            : (!no_tenant_stage ? (uint32_t)std::min<size_t>(max_blob, ajx::kMaxTenantStageBytes) : 0u);
             HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                          d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
                                          w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
@@ -559,6 +558,9 @@ int authjx_debug_tenant_stage(authjx_ctx* ctx, int on) {
     ctx->no_tenant_stage = on ? 0 : 1;
     return AUTHJX_OK;
 }
+
+// profiling: a compiled ruleset's device blob size in bytes (what the kernels stage in LDS)
+uint32_t authjx_debug_blob_bytes(const authjx_ruleset* rs) { return rs ? (uint32_t)rs->c.blob.size() : 0u; }
 
 int authjx_set_exact_scan(authjx_ctx* ctx, int force) {
     if (!ctx) return AUTHJX_EINVAL;

@@ -197,7 +197,9 @@ struct RulesetHdr {
     uint32_t pad1[3];
     uint32_t off_modifiers;     // Modifier[n_modifiers]
     uint32_t n_modifiers;
-    uint32_t pad2[6];
+    uint32_t hot_bytes;         // [0, hot_bytes): every table the single-pass kernels read
+                                // (selectors, components, modifiers follow: exact scan only)
+    uint32_t pad2[5];
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
     uint64_t unsupported[2];    // pattern p can not be decided on the device

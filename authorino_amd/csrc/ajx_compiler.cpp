@@ -731,12 +731,6 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         }
     }
     hdr.n_modifiers = (uint32_t)mods.size();
-    hdr.off_modifiers = (uint32_t)b.align16();
-    b.append(mods.data(), mods.size() * sizeof(Modifier));
-    hdr.off_selectors = (uint32_t)b.align16();
-    b.append(sels.data(), sels.size() * sizeof(Selector));
-    hdr.off_components = (uint32_t)b.align16();
-    b.append(comps.data(), comps.size() * sizeof(Component));
     hdr.off_code = (uint32_t)b.align16();
     b.append(code.data(), code.size() * sizeof(uint32_t));
     if (forest) {
@@ -774,6 +768,14 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     }
     hdr.off_patterns = (uint32_t)b.align16();
     b.append(pats.data(), pats.size() * sizeof(Pattern));
+    // the exact scan's tables last: the multi-tenant kernel stages only [0, hot_bytes)
+    hdr.hot_bytes = (uint32_t)b.align16();
+    hdr.off_modifiers = (uint32_t)b.align16();
+    b.append(mods.data(), mods.size() * sizeof(Modifier));
+    hdr.off_selectors = (uint32_t)b.align16();
+    b.append(sels.data(), sels.size() * sizeof(Selector));
+    hdr.off_components = (uint32_t)b.align16();
+    b.append(comps.data(), comps.size() * sizeof(Component));
     b.align16();
     if (b.blob.size() > 0xFFFFFFFFull) return AUTHJX_ELIMIT;
     hdr.magic = kMagic;

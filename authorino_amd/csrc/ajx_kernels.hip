@@ -381,7 +381,8 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
 // set_of_req; the caller buckets requests by AuthConfig, so a workgroup's requests form a
 // few runs of one ruleset each). The workgroup finds its runs (a run starts where the
 // ruleset differs from the previous work-item's) and copies the blobs of its first runs
-// into LDS, as many as fit the staging region; a wave whose requests all fall in staged
+// into LDS — each blob's hot prefix, [0, hot_bytes), which holds every table this kernel
+// reads — as many as fit the staging region; a wave whose requests all fall in staged
 // runs reads every table from LDS (each lane from its own run's copy), any other wave
 // reads them from global memory. Dynamic LDS: [staging region (ring_off bytes)] [rings].
 constexpr uint32_t kTenantRuns = 8;  // runs a workgroup may stage
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     const uint32_t nr = nrun < kTenantRuns ? nrun : kTenantRuns;
     for (uint32_t j = 0; j < nr; j++) {
         const uint8_t* g = sets[s_rsid[j]];
-        const uint32_t bytes = reinterpret_cast<const RulesetHdr*>(g)->total_bytes;  // (a multiple of 16)
+        const uint32_t bytes = reinterpret_cast<const RulesetHdr*>(g)->hot_bytes;  // (a multiple of 16)
         if (off + bytes > ring_off) break;
         const uint4* src = reinterpret_cast<const uint4*>(g);
         for (uint32_t i = t; i < bytes / 16u; i += blockDim.x) s_stage[off / 16u + i] = src[i];
@@ -979,8 +980,9 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
             hipLaunchKernelGGL((ajx_scan_fused<true, false>), dim3(grid), dim3(block), lds, stream, d_sets,
                                d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids,
                                d_tri, d_err, d_bm, stride, ring_off, d_perm);
-    } else if (d_set_of_req && shared_blob_bytes && shared_blob_bytes <= kMaxTenantStageBytes) {
-        // multi-tenant batch: shared_blob_bytes = the largest ruleset blob of the batch;
+    } else if (d_set_of_req && shared_blob_bytes) {
+        // multi-tenant batch (shared_blob_bytes != 0: staging on): each workgroup stages its
+        // runs' rulesets, those that fit (ajx_scan_fused_tenant);
         // 4-wave workgroups, so more of them fall inside one AuthConfig's bucket
         // (staging region: the tenant budget less room for the kernel's static LDS, so
         // four groups still fit a CU)
