@@ -158,6 +158,7 @@ struct KeySlot {
 static_assert(sizeof(KeySlot) == 16, "KeySlot layout");
 constexpr uint32_t kEmptySlot = 0xFFFFFFFFu;
 constexpr uint32_t kMaxKeySlotsLog2 = 9;
+constexpr uint32_t kKeyProbes = 4;  // the table is grown until every key is this close to home
 
 AJX_BLOB_HD inline uint32_t key_slot_hash(uint64_t sig, uint32_t klen, uint32_t parent, uint32_t log2) {
     uint32_t x = (uint32_t)sig ^ (((uint32_t)(sig >> 32) << 13) | ((uint32_t)(sig >> 32) >> 19)) ^ (klen << 24) ^
@@ -199,7 +200,8 @@ struct RulesetHdr {
     uint32_t n_modifiers;
     uint32_t hot_bytes;         // [0, hot_bytes): every table the single-pass kernels read
                                 // (selectors, components, modifiers follow: exact scan only)
-    uint32_t pad2[5];
+    uint32_t key_probes;        // every key sits within key_probes slots of its home slot
+    uint32_t pad2[4];
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
     uint64_t unsupported[2];    // pattern p can not be decided on the device

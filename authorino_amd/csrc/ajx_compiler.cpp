@@ -686,22 +686,33 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 tc.push_back(ch);
             }
         }
-        // key table: load factor <= 1/2
+        // key table (linear probing): load factor <= 1/2, then grown until every key sits
+        // within kKeyProbes slots of its home slot (up to kMaxKeySlotsLog2); key_probes, the
+        // largest distance, bounds every lookup's probe sequence (a wave runs its longest
+        // lane's sequence: a miss no longer walks to the end of its cluster)
         uint32_t log2 = 4;
         while ((1u << log2) < 2 * tc.size() && log2 < kMaxKeySlotsLog2) log2++;
-        std::vector<KeySlot> slots(1u << log2);
-        for (KeySlot& k : slots) { k.sig = 0; k.meta = kEmptySlot; k.key_off = 0; }
-        for (size_t i = 0; i < trie.size(); i++) {
-            for (uint32_t j = 0; j < tn[i].n_children; j++) {
-                const TrieChild& ch = tc[tn[i].child_begin + j];
-                uint32_t at = key_slot_hash(ch.sig, ch.key_len, (uint32_t)i, log2);
-                while (slots[at].meta != kEmptySlot) at = (at + 1) & ((1u << log2) - 1);
-                slots[at].sig = ch.sig;
-                slots[at].meta = ch.key_len | ((uint32_t)i << 16) | (ch.node << 24);
-                slots[at].key_off = ch.key_off;
+        std::vector<KeySlot> slots;
+        uint32_t probes = 1;
+        for (;;) {
+            slots.assign(1u << log2, KeySlot{0, kEmptySlot, 0});
+            probes = 1;
+            for (size_t i = 0; i < trie.size(); i++) {
+                for (uint32_t j = 0; j < tn[i].n_children; j++) {
+                    const TrieChild& ch = tc[tn[i].child_begin + j];
+                    uint32_t at = key_slot_hash(ch.sig, ch.key_len, (uint32_t)i, log2), dist = 1;
+                    while (slots[at].meta != kEmptySlot) at = (at + 1) & ((1u << log2) - 1), dist++;
+                    slots[at].sig = ch.sig;
+                    slots[at].meta = ch.key_len | ((uint32_t)i << 16) | (ch.node << 24);
+                    slots[at].key_off = ch.key_off;
+                    probes = std::max(probes, dist);
+                }
             }
+            if (probes <= kKeyProbes || log2 >= kMaxKeySlotsLog2) break;
+            log2++;
         }
         hdr.key_slots_log2 = log2;
+        hdr.key_probes = probes;
         hdr.n_trie_nodes = (uint32_t)tn.size();
         hdr.off_trie_nodes = (uint32_t)b.align16();
         b.append(tn.data(), tn.size() * sizeof(TrieNode));

@@ -322,7 +322,7 @@ AJX_HD bool scan_doc_ev(const uint8_t* blob, const Tables& tab, const uint8_t* d
     s.tn = tab.tn;
     s.tc = tab.tc;
     s.ks = tab.ks;
-    s.ks_log2 = h->key_slots_log2;
+    s.ks_meta = h->key_slots_log2 | h->key_probes << 8;
     s.lits = blob + h->off_literals;
     s.d = d;
     s.row = row;

@@ -128,8 +128,8 @@ struct WinRing {
 struct Scan {
     const TrieNode* tn;
     const TrieChild* tc;
-    const KeySlot* ks;  // key table (1 << ks_log2 slots)
-    uint32_t ks_log2;
+    const KeySlot* ks;  // key table (1 << (ks_meta & 0xFF) slots)
+    uint32_t ks_meta;   // log2 of the slot count | key_probes << 8 (one register for both)
     const uint8_t* lits;
     const uint8_t* d;
     RowRef row;     // capture row (header + records)
@@ -358,36 +358,40 @@ struct Scan {
         uint64_t sig = tail8(i);
         if (klen < 8) sig = klen ? sig >> (8 * (8 - klen)) : 0ull;
 #endif
-        const uint32_t want = (klen & 0xFFFFu) | (parent << 16), mask = (1u << ks_log2) - 1u;
-        uint32_t at = key_slot_hash(sig, klen, parent, ks_log2);
-        for (uint32_t probe = 0; probe <= mask; probe++, at = (at + 1) & mask) {
-            const KeySlot slot = ks[at];
+        if (klen > 0xFFFFu) return;
+        const uint32_t log2 = ks_meta & 0xFFu, want = klen | (parent << 16), mask = (1u << log2) - 1u;
+        const uint32_t at = key_slot_hash(sig, klen, parent, log2);
+        // every key of the table sits within key_probes slots of its home (the compiler grows
+        // the table for that), so the probe sequence is bounded by it, not by an empty slot
+        uint32_t pos = at;
+        for (uint32_t probe = 0; probe < (ks_meta >> 8); probe++, pos = (pos + 1) & mask) {
+            const KeySlot slot = ks[pos];
             if (slot.meta == kEmptySlot) return;
-            if (slot.sig != sig || (slot.meta & 0xFFFFFFu) != want || klen > 0xFFFFu) continue;
-            bool eq = true;
-            const uint8_t* kl = lits + slot.key_off;
-            const uint32_t a0 = k0 + (wa - (uint32_t)bpos);  // ring position of the key's first byte
-#ifdef AJX_ABLATE_KEY_NOCMP
-            if (false) {
-#else
-            if (a0 + 64u >= wa) {  // the key began in the ring's windows: compare from LDS
-#endif
-                for (uint32_t k = 0; k + 8 < klen; k += 4) {
-                    const uint32_t r = klen - 8 - k;
-                    const uint32_t m = r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
-                    if ((ring.u32(a0 + k) ^ load_u32_any(kl + k)) & m) { eq = false; break; }
-                }
-            } else {
-#ifndef AJX_ABLATE_KEY_NOCMP
-                for (uint32_t k = 0; k + 8 < klen; k++)
-                    if (d[k0 + k] != kl[k]) { eq = false; break; }
-#endif
-            }
-            if (eq) { pending = slot.meta >> 24; return; }
+            if (slot.sig != sig || (slot.meta & 0xFFFFFFu) != want) continue;
+            if (klen <= 8 || key_rest_equal(k0, klen, slot.key_off)) { pending = slot.meta >> 24; return; }
 #ifdef AJX_ABLATE_KEY_PROBE1
             return;
 #endif
         }
+    }
+    // the bytes of a key [k0, k0 + klen) before its last 8 equal the literal at key_off
+    AJX_HD bool key_rest_equal(uint32_t k0, uint32_t klen, uint32_t key_off) const {
+        const uint8_t* kl = lits + key_off;
+        const uint32_t a0 = k0 + (wa - (uint32_t)bpos);  // ring position of the key's first byte
+#ifdef AJX_ABLATE_KEY_NOCMP
+        return true;
+#endif
+        if (a0 + 64u >= wa) {  // the key began in the ring's windows: compare from LDS
+            for (uint32_t k = 0; k + 8 < klen; k += 4) {
+                const uint32_t r = klen - 8 - k;
+                const uint32_t m = r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
+                if ((ring.u32(a0 + k) ^ load_u32_any(kl + k)) & m) return false;
+            }
+            return true;
+        }
+        for (uint32_t k = 0; k + 8 < klen; k++)
+            if (d[k0 + k] != kl[k]) return false;
+        return true;
     }
 
     // a string value closed at block offset i (state X_VALUE / X_VALUE_OR_CLOSE)
@@ -620,7 +624,7 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     s.tn = tab.tn;
     s.tc = tab.tc;
     s.ks = tab.ks;
-    s.ks_log2 = h->key_slots_log2;
+    s.ks_meta = h->key_slots_log2 | h->key_probes << 8;
     s.lits = blob + h->off_literals;
     s.d = d;
     s.row = row;

@@ -1,5 +1,6 @@
-# one iteration: GPU parity tests, then the default kernel on c2 / c3
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || exit $?
-timeout -k 10 200 python scripts/ablate_scan.py c2 1048576 0 > gpurun_out/variants.log 2>&1 || exit $?
-timeout -k 10 200 python scripts/ablate_scan.py c3 1048576 0 >> gpurun_out/variants.log 2>&1 || exit $?
+# quick check of the current tree: GPU suite, then bench lines for c2..c5 (no CPU legs)
+cd $GRAFT_REPO_ROOT && O=gpurun_out/${1:-quick} && mkdir -p $O && export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit $?
+for w in c2 c3 c4 c5; do
+  timeout -k 10 300 python bench.py --workload $w --no-cpu --no-pcie > $O/bench_$w.log 2>&1 || exit $?
+done
