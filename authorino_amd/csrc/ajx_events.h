@@ -173,9 +173,11 @@ struct EvScan : Scan {
         depth++;
         const uint64_t bit = 1ull << depth;
         is_arr = c == '[' ? is_arr | bit : is_arr & ~bit;
+        top_arr = c == '[' ? 1u : 0u;
         const uint32_t live = node != kNoNode && tn[node].n_children ? node : kNoNode;
         if (live != kNoNode && depth > kFastDepth) return false;
         set_node(depth, live);
+        top_node = live;
         if (s >= 0) {
             found |= 1ull << s;  // first match in document order wins
             if (ncap >= 2) return false;
@@ -335,6 +337,8 @@ AJX_HD bool scan_doc_ev(const uint8_t* blob, const Tables& tab, const uint8_t* d
     s.oq = 0;
     s.carry_oq = s.last_oq = 0;
     s.is_arr = 0;
+    s.top_arr = 0;
+    s.top_node = 0;  // (the root's node)
     s.nodes_lo = s.nodes_hi = ~0ull;
     s.found = 0;
     s.depth = 0;

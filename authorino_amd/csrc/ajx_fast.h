@@ -145,6 +145,8 @@ struct Scan {
     uint32_t last_oq;
 
     uint64_t is_arr;    // bit k: container at depth k (1-based) is an array
+    uint32_t top_arr;   // (is_arr >> depth) & 1, kept up to date at every push and pop
+    uint32_t top_node;  // node_at(depth), kept likewise
     uint64_t nodes_lo;  // trie node per depth 1..8 (kNoNode = none)
     uint64_t nodes_hi;  // depths 9..16
     uint64_t found;     // selectors captured
@@ -196,13 +198,13 @@ struct Scan {
         nodes_lo = k < 8 ? (lo & ~m) | x : lo;
         nodes_hi = k < 8 ? hi : (hi & ~m) | x;
     }
-    AJX_HD bool top_is_arr() const { return (is_arr >> depth) & 1; }
+    AJX_HD bool top_is_arr() const { return top_arr != 0; }
     // trie node of the value about to start (key for objects, element index for arrays)
     AJX_HD uint32_t value_node() const {
         if (depth == 0) return 0;
         if (!top_is_arr()) return pending;
         if (!narr) return kNoNode;  // no live array open: the element is off every path
-        const uint32_t parent = node_at(depth);
+        const uint32_t parent = top_node;
         if (parent == kNoNode || !(tn[parent].flags & 1)) return kNoNode;
         uint32_t h;
         if (narr >= 2 && (arr1 & 0xFF) == depth) h = arr1 >> 8;
@@ -238,8 +240,10 @@ struct Scan {
         depth++;
         const uint64_t bit = 1ull << depth;
         is_arr = c == '[' ? is_arr | bit : is_arr & ~bit;
+        top_arr = c == '[' ? 1u : 0u;
         if (node == kNoNode) {  // off every selector path (the common case)
             set_node(depth, kNoNode);
+            top_node = kNoNode;
             st = c == '[' ? X_VALUE_OR_CLOSE : X_KEY_OR_CLOSE;
             return true;
         }
@@ -247,6 +251,7 @@ struct Scan {
         const uint32_t live = tn[node].n_children ? node : kNoNode;
         if (live != kNoNode && depth > kFastDepth) return false;
         set_node(depth, live);
+        top_node = live;
         if (s >= 0) {
             found |= 1ull << s;  // first match in document order wins
             if (ncap >= 2) return false;
@@ -286,6 +291,8 @@ struct Scan {
             if ((at & 0xFF) == depth) narr--;
         }
         depth--;
+        top_arr = (uint32_t)(is_arr >> depth) & 1u;
+        top_node = node_at(depth);
         st = depth == 0 ? X_DONE : X_COMMA_OR_CLOSE;
         element_done();  // the container was an element of its parent array
     }
@@ -343,7 +350,7 @@ struct Scan {
 #ifdef AJX_ABLATE_FAST_NOKEYS
         return;  // profiling: no selector ever matches (the grammar walk alone)
 #endif
-        const uint32_t parent = node_at(depth);
+        const uint32_t parent = top_node;
         if (parent == kNoNode) return;
         // (a live node always has children: open_container stores only those)
         str_open = open_before(i);
@@ -361,6 +368,25 @@ struct Scan {
         if (klen > 0xFFFFu) return;
         const uint32_t log2 = ks_meta & 0xFFu, want = klen | (parent << 16), mask = (1u << log2) - 1u;
         const uint32_t at = key_slot_hash(sig, klen, parent, log2);
+#ifdef AJX_KEY_UNROLL  // (experiment: the key_probes <= 4 slots read at once, no loop)
+        if ((ks_meta >> 8) <= kKeyProbes) {
+            uint32_t cand = 0, node = kNoNode, koff = 0;
+#pragma unroll
+            for (int q = (int)kKeyProbes - 1; q >= 0; q--) {
+                const KeySlot sl = ks[(at + (uint32_t)q) & mask];
+                const bool c = (uint32_t)q < (ks_meta >> 8) && sl.meta != kEmptySlot && sl.sig == sig &&
+                               (sl.meta & 0xFFFFFFu) == want;
+                cand += c ? 1u : 0u;
+                node = c ? sl.meta >> 24 : node;
+                koff = c ? sl.key_off : koff;
+            }
+            if (cand == 1) {
+                if (klen <= 8 || key_rest_equal(k0, klen, koff)) pending = node;
+                return;
+            }
+            if (cand == 0) return;
+        }
+#endif
         // every key of the table sits within key_probes slots of its home (the compiler grows
         // the table for that), so the probe sequence is bounded by it, not by an empty slot
         uint32_t pos = at;
@@ -637,6 +663,8 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     s.oq = 0;
     s.carry_oq = s.last_oq = 0;
     s.is_arr = 0;
+    s.top_arr = 0;
+    s.top_node = 0;  // (the root's node)
     s.nodes_lo = s.nodes_hi = ~0ull;
     s.found = 0;
     s.depth = 0;
