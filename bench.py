@@ -384,13 +384,14 @@ def main():
     if phase:
         algo_bytes += w.n * len(sel.paths) * 12
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, traffic_note = None, None
     try:
         with open(args.pmc_json) as f:
             pmc = json.load(f).get(args.workload, {})
         # (measured by scripts/pmc_traffic.py on the same workload, size and kernel)
         if pmc.get("n") == w.n and args.kernel_mode in (0, 20) and (args.kernel_mode == 20) == ("lane" in pmc.get("kernel", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
+            traffic_note = pmc.get("note")
     except (OSError, ValueError):
         pass
 
@@ -477,6 +478,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
+                "traffic_note": traffic_note,
                 "kernel_ms": kern_ms,
                 **({"note": "kernel_ms is the whole step's event time, decision all-gather included"}
                    if gather else {}),

@@ -8,6 +8,8 @@ for w in c2 c3 c4 c5; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_$w -o $w -- python -u bench.py --no-cpu --no-pcie --workload $w --steps 10 > $O/prof_$w.log 2>&1 || exit $?
 done
 rm -f $O/pmc_traffic.json
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_calib -o f -- python -u bench.py --no-cpu --no-pcie --workload c2 --kernel-mode 1 --steps 2 --warmup 1 > $O/pmc_fetch_calib.log 2>&1 || exit $?
+python scripts/fetch_calibration.py $O/pmc_fetch_calib c2 1048576 $O/pmc_traffic.json > $O/fetch_calibration.log 2>&1 || exit $?
 for w in c2 c3 c4 c5; do
   n=1048576; [ $w = c4 ] && n=2097152; [ $w = c5 ] && n=2097152
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$w -o f -- python -u bench.py --no-cpu --no-pcie --workload $w --steps 2 --warmup 1 > $O/pmc_fetch_$w.log 2>&1 || exit $?

@@ -7,9 +7,9 @@ launch of the dominant kernel, merged per workload into pmc_traffic.json at the 
 FETCH_SIZE / WRITE_SIZE are reported in KiB. MI355X_MICROARCH.md (HBM/rocprofv3 section):
 FETCH_SIZE counts exactly half the bytes of a wide coalesced streaming read on gfx950;
 other access widths are uncalibrated. The dominant kernel reads each document with
-per-lane 16-byte loads (one document per lane), so both the raw value and the doubled
-value are recorded; `hbm_bytes_per_launch` uses the raw FETCH + WRITE sum (the
-conservative, smaller figure) and the note says so.
+per-lane 16-byte loads (one document per lane): scripts/fetch_calibration.py measures the
+factor for that shape (exact bytes of the loads-only ablation / its FETCH_SIZE), and
+`hbm_bytes_per_launch` = FETCH_SIZE x factor + WRITE_SIZE (raw values kept beside it).
 """
 import csv
 import glob
@@ -33,17 +33,6 @@ def main():
     kernel = sys.argv[6] if len(sys.argv) > 6 else "ajx_scan_fused"
     fb, nf = per_launch(fetch_dir, "FETCH_SIZE", kernel)
     wb, nw = per_launch(write_dir, "WRITE_SIZE", kernel)
-    res = {
-        "workload": workload,
-        "n": n,
-        "kernel": kernel,
-        "fetch_bytes_per_launch_raw": fb,
-        "write_bytes_per_launch": wb,
-        "launches": [nf, nw],
-        "hbm_bytes_per_launch": (fb or 0) + (wb or 0),
-        "note": "FETCH_SIZE+WRITE_SIZE (KiB*1024), median over launches, raw (not doubled): per-lane 16-B "
-                "loads are outside the guide's calibrated access shapes",
-    }
     try:
         with open(out) as f:
             allw = json.load(f)
@@ -51,6 +40,20 @@ def main():
             allw = {allw["workload"]: allw}
     except (OSError, ValueError):
         allw = {}
+    # the factor scripts/fetch_calibration.py measured for this access shape (else raw)
+    k = (allw.get("calibration") or {}).get("factor")
+    res = {
+        "workload": workload,
+        "n": n,
+        "kernel": kernel,
+        "fetch_bytes_per_launch_raw": fb,
+        "fetch_calibration": k,
+        "write_bytes_per_launch": wb,
+        "launches": [nf, nw],
+        "hbm_bytes_per_launch": (fb or 0) * (k or 1.0) + (wb or 0),
+        "note": ("FETCH_SIZE x calibration (loads-only ablation, same shape) + WRITE_SIZE" if k else
+                 "FETCH_SIZE+WRITE_SIZE raw (uncalibrated)") + ", KiB*1024, median over launches",
+    }
     allw[workload] = res
     with open(out, "w") as f:
         json.dump(allw, f, indent=1)
