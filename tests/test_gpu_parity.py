@@ -255,6 +255,29 @@ def test_multi_tenant_c4(ctx):
     assert 0 < (tri == 1).sum() < w.n
 
 
+def test_multi_tenant_runs_staged(ctx):
+    """The multi-tenant kernel's run staging: requests of 600 AuthConfigs in runs of ~100
+    (2-4 runs per workgroup, one or two staged in LDS, the rest from global memory), and
+    an unsorted copy of the same batch (a run per request), against the oracle."""
+    from authorino_amd import workloads
+
+    w = workloads.make("c4", n=60000, seed=43)
+    sid = (w.set_of_req.astype(np.int64) % 600)
+    order = np.argsort(sid, kind="stable")
+    used = np.unique(sid)
+    sets = [ctx.compile_expression(w.exprs[i]) for i in used]
+    osets = [O.Ruleset.from_expression(w.exprs[i]) for i in used]
+    remap = np.searchsorted(used, sid).astype(np.uint32)
+    for perm in (order, np.random.default_rng(3).permutation(w.n)):
+        offs, lens, sor = w.offs[perm], w.lens[perm], remap[perm]
+        tri, err, bm = ctx.eval_host_arena(sets, w.arena, offs, lens, set_of_req=sor)
+        otri, oerr, obm = _oracle(None, w.arena, offs, lens, set_of_req=sor, sets=osets)
+        assert (tri == 3).sum() == 0
+        assert np.array_equal(tri, otri)
+        assert np.array_equal(err, oerr)
+        assert np.array_equal(bm, obm)
+
+
 def test_select_values_match_oracle(ctx):
     """authjx_select_batch (gjson.Get spans for response selectors)
     against the oracle's Get on random documents (escapes, numbers, containers, missing
