@@ -77,6 +77,8 @@ AJX_HD uint32_t ctz64f(uint64_t x) { return (uint32_t)__builtin_ctzll(x); }
 AJX_HD uint32_t hibit64f(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
 AJX_HD uint32_t popc64f(uint64_t x) { return (uint32_t)__builtin_popcountll(x); }
 AJX_HD uint64_t below64f(uint32_t i) { return i >= 64 ? ~0ull : ((1ull << i) - 1ull); }
+AJX_HD uint64_t lt64(uint32_t i) { return (1ull << i) - 1ull; }  // bits below i, i < 64
+AJX_HD uint64_t upto64(uint32_t i) { return ~0ull >> (63u - i); }  // bits 0..i, i < 64
 
 // The document window ring of one work-item: the current and the previous 64-byte
 // window. Chunk j (16 B) of the ring — j = (A >> 4) & 7 for the position A relative to
@@ -170,11 +172,11 @@ struct Scan {
     AJX_HD uint32_t byte_at(uint32_t i) const { return ring.u8(wa + i); }
     // opening quote of the string whose closing quote is at window offset i
     AJX_HD uint32_t open_before(uint32_t i) const {
-        const uint64_t ob = oq & below64f(i);
+        const uint64_t ob = oq & lt64(i);  // (i < 64: a token's window offset)
         return ob ? (uint32_t)(bpos + (int32_t)hibit64f(ob)) : carry_oq;
     }
     AJX_HD uint32_t last_bs_before(uint32_t i) const {
-        const uint64_t mb = mbs & below64f(i);
+        const uint64_t mb = mbs & lt64(i);
         return mb ? (uint32_t)(bpos + (int32_t)hibit64f(mb)) : carry_bs;
     }
 
@@ -578,13 +580,13 @@ struct Scan {
         while (toks) {
             const uint32_t i = ctz64f(toks);
             toks &= toks - 1;
-            const uint64_t g = ns & below64f(i) & ~below;
+            const uint64_t g = ns & lt64(i) & ~below;
             if (g) {
                 if (gap_cnt == 0) gap_first = (uint32_t)(bp + (int32_t)ctz64f(g));
                 gap_last = (uint32_t)(bp + (int32_t)hibit64f(g));
                 gap_cnt += popc64f(g);
             }
-            below = below64f(i + 1);
+            below = upto64(i);
             token(byte_at(i), i);
             if (st >= X_DONE) return;
             // compact JSON: the ':' right after a key and the ',' right after a value are
@@ -598,19 +600,19 @@ struct Scan {
                 if (colon || comma) {
                     st = (colon || top_is_arr()) ? X_VALUE : X_KEY;
                     toks &= toks - 1;
-                    below = below64f(nb + 1);
+                    below = upto64(nb);
                     // the opening quote right after the ':' and its closing quote in this
                     // window (nothing inside a string is a token: it is the next token)
                     if (colon && nb + 1 < 64 && ((oq >> (nb + 1)) & 1u) && toks) {
                         const uint32_t j = ctz64f(toks);
                         toks &= toks - 1;
-                        below = below64f(j + 1);
+                        below = upto64(j);
                         value_string(j);
                         const uint32_t nb2 = j + 1;
                         if (nb2 < 64 && ((toks >> nb2) & 1u) && byte_at(nb2) == ',') {
                             st = top_is_arr() ? X_VALUE : X_KEY;
                             toks &= toks - 1;
-                            below = below64f(nb2 + 1);
+                            below = upto64(nb2);
                         }
                     }
                 }
