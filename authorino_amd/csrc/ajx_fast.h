@@ -169,7 +169,11 @@ struct Scan {
         if (a < 0) return ring.u64(0) << (8 * (uint32_t)(-a));  // (before the first block: zeros)
         return ring.u64((uint32_t)a);
     }
-    AJX_HD uint32_t byte_at(uint32_t i) const { return ring.u8(wa + i); }
+    // window byte i (< 64); wa is a multiple of 64, so its chunk is (wa's half of the
+    // ring) | i / 16
+    AJX_HD uint32_t byte_at(uint32_t i) const {
+        return ring.base[(((wa >> 4) & 4u) | (i >> 4)) * ring.cstride + ring.lane16 + (i & 15u)];
+    }
     // opening quote of the string whose closing quote is at window offset i
     AJX_HD uint32_t open_before(uint32_t i) const {
         const uint64_t ob = oq & lt64(i);  // (i < 64: a token's window offset)
@@ -593,7 +597,7 @@ struct Scan {
             // taken in the same iteration, and so is a member's string value that opens
             // right after its ':' ("key":"value", — one iteration per member)
             const uint32_t nb = i + 1;
-            if (nb < 64 && ((toks >> nb) & 1u)) {
+            if (toks & (2ull << i)) {  // (a token at i + 1; none when i = 63)
                 const uint32_t c2 = byte_at(nb);
                 const bool colon = st == X_COLON && c2 == ':';
                 const bool comma = st == X_COMMA_OR_CLOSE && c2 == ',';
@@ -603,13 +607,13 @@ struct Scan {
                     below = upto64(nb);
                     // the opening quote right after the ':' and its closing quote in this
                     // window (nothing inside a string is a token: it is the next token)
-                    if (colon && nb + 1 < 64 && ((oq >> (nb + 1)) & 1u) && toks) {
+                    if (colon && (oq & (4ull << i)) && toks) {
                         const uint32_t j = ctz64f(toks);
                         toks &= toks - 1;
                         below = upto64(j);
                         value_string(j);
                         const uint32_t nb2 = j + 1;
-                        if (nb2 < 64 && ((toks >> nb2) & 1u) && byte_at(nb2) == ',') {
+                        if ((toks & (2ull << j)) && byte_at(nb2) == ',') {
                             st = top_is_arr() ? X_VALUE : X_KEY;
                             toks &= toks - 1;
                             below = upto64(nb2);
