@@ -58,6 +58,19 @@ AJX_HD uint32_t gather4(uint32_t f) {  // 0x80-per-byte flags -> 4-bit mask
     uint32_t x = f >> 7;
     return (x | (x >> 7) | (x >> 14) | (x >> 21)) & 0xFu;
 }
+// the 0x80-per-byte flags of 16 bytes (f_i: bytes 4i..4i+3) -> 16-bit mask, bit 4i + j =
+// byte j of f_i: the four dwords' flags are merged into one dword (byte j, bit i), its
+// nibbles packed into a 4 x 4 bit matrix and transposed with two delta swaps
+AJX_HD uint32_t gather16(uint32_t f0, uint32_t f1, uint32_t f2, uint32_t f3) {
+    const uint32_t y = (f0 >> 7) | (f1 >> 6) | (f2 >> 5) | (f3 >> 4);
+    const uint32_t t0 = (y | (y >> 4)) & 0x00FF00FFu;
+    uint32_t z = (t0 | (t0 >> 8)) & 0xFFFFu;  // bit 4j + i
+    uint32_t t = (z ^ (z >> 3)) & 0x0A0Au;
+    z ^= t ^ (t << 3);
+    t = (z ^ (z >> 6)) & 0x00CCu;
+    z ^= t ^ (t << 6);
+    return z;  // bit 4i + j
+}
 AJX_HD uint32_t ctz32(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
 AJX_HD uint32_t popc32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 AJX_HD uint32_t hibit32(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
@@ -509,18 +522,19 @@ struct Scan {
         for (int j = 0; j < 4; j++) {
             const Block16 x4 = blk[j];
             ring.put(a + 16u * (uint32_t)j, x4);
-            uint32_t q16 = 0, b16 = 0, s16 = 0, w16 = 0;
+            uint32_t qf[4], bf[4], sf[4], wf[4];  // (0x80-per-byte flags; unrolled: registers)
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const uint32_t x = k == 0 ? x4.x : k == 1 ? x4.y : k == 2 ? x4.z : x4.w;
                 const uint32_t lx = x | 0x20202020u;
-                q16 |= gather4(eq_bytes(x, 0x22222222u)) << (4 * k);
-                b16 |= gather4(eq_bytes(x, 0x5C5C5C5Cu)) << (4 * k);
-                s16 |= gather4(eq_bytes(lx, 0x7B7B7B7Bu) | eq_bytes(lx, 0x7D7D7D7Du) | eq_bytes(x, 0x3A3A3A3Au) |
-                               eq_bytes(x, 0x2C2C2C2Cu))
-                       << (4 * k);
-                w16 |= gather4(le20_bytes(x)) << (4 * k);
+                qf[k] = eq_bytes(x, 0x22222222u);
+                bf[k] = eq_bytes(x, 0x5C5C5C5Cu);
+                sf[k] = eq_bytes(lx, 0x7B7B7B7Bu) | eq_bytes(lx, 0x7D7D7D7Du) | eq_bytes(x, 0x3A3A3A3Au) |
+                        eq_bytes(x, 0x2C2C2C2Cu);
+                wf[k] = le20_bytes(x);
             }
+            const uint32_t q16 = gather16(qf[0], qf[1], qf[2], qf[3]), b16 = gather16(bf[0], bf[1], bf[2], bf[3]);
+            const uint32_t s16 = gather16(sf[0], sf[1], sf[2], sf[3]), w16 = gather16(wf[0], wf[1], wf[2], wf[3]);
             mq |= (uint64_t)q16 << (16 * j);
             mb |= (uint64_t)b16 << (16 * j);
             mst |= (uint64_t)s16 << (16 * j);
