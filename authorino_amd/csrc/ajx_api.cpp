@@ -48,6 +48,8 @@ struct Workspace {
     size_t rows_cap = 0;         // in u64
     uint32_t* d_perm = nullptr;  // length-bucketed request order (+ 2 x 1024 + 1 u32 histogram)
     uint32_t perm_cap = 0;
+    uint32_t* d_tier = nullptr;  // the row kernel's tier lists: 2 x ([0] count + n ids)
+    uint32_t tier_cap = 0;
     // the capture rows in d_rows: written by the last single-ruleset, full evaluation of
     // rows_rs over rows_n requests on this stream (nullptr: none usable)
     const authjx_ruleset* rows_rs = nullptr;
@@ -128,6 +130,7 @@ void destroy_workspace(Workspace* w) {
     if (w->d_slow) (void)hipFree(w->d_slow);
     if (w->d_rows) (void)hipFree(w->d_rows);
     if (w->d_perm) (void)hipFree(w->d_perm);
+    if (w->d_tier) (void)hipFree(w->d_tier);
     if (w->ev0) (void)hipEventDestroy(w->ev0);
     if (w->ev1) (void)hipEventDestroy(w->ev1);
     delete w;
@@ -164,7 +167,7 @@ int ensure_sets(Workspace* w, int device, const authjx_ruleset* const* sets, uin
 int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
     // (rows for whole waves: the fused kernels' wave-interleaved layout)
     const size_t rows_need = (size_t)((n + 63u) & ~63u) * row_stride;
-    if (n <= w->slow_cap && n <= w->perm_cap && rows_need <= w->rows_cap) return AUTHJX_OK;
+    if (n <= w->slow_cap && n <= w->perm_cap && n <= w->tier_cap && rows_need <= w->rows_cap) return AUTHJX_OK;
     HIP_OK(hipStreamSynchronize(w->stream));
     w->rows_rs = nullptr;
     if (n > w->slow_cap) {
@@ -180,6 +183,13 @@ int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
         w->perm_cap = 0;
         HIP_OK(hipMalloc(&w->d_perm, ((size_t)n + 4096) * sizeof(uint32_t)));
         w->perm_cap = n;
+    }
+    if (n > w->tier_cap) {
+        if (w->d_tier) (void)hipFree(w->d_tier);
+        w->d_tier = nullptr;
+        w->tier_cap = 0;
+        HIP_OK(hipMalloc(&w->d_tier, 2 * ((size_t)n + 1) * sizeof(uint32_t)));
+        w->tier_cap = n;
     }
     if (rows_need > w->rows_cap) {
         if (w->d_rows) (void)hipFree(w->d_rows);
@@ -217,6 +227,11 @@ int batch_done(Workspace* w, const authjx_ruleset* const* sets, uint32_t n_sets)
 }  // namespace
 
 extern "C" {
+
+#ifndef AJX_SRC_HASH
+#define AJX_SRC_HASH "unknown"
+#endif
+const char* authjx_build_hash(void) { return AJX_SRC_HASH; }
 
 int authjx_device_count(void) {
     int n = 0;
@@ -377,8 +392,13 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     for (uint32_t i = 0; i < n_sets; i++)
         mods = mods || reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->n_modifiers != 0 ||
                (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagBufs) != 0;
+    // the row kernel (ajx_row.h; default for a batch over one ruleset with row tables);
+    // ablate 40 keeps the token-scanner single-pass kernel, 41 is the row scan alone
+    const ajx::RulesetHdr* h0 = reinterpret_cast<const ajx::RulesetHdr*>(sets[0]->c.blob.data());
+    const bool row = fast_tables && n_sets == 1 && (ablate == 0 || ablate == 41) && h0->off_row != 0 &&
+                     h0->n_selectors <= 64 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes;
     // capture rows kept for authjx_select_from_eval_device: one ruleset, a full kernel
-    const bool full = ablate == 0 || ablate == 20 || ablate == 31 || (ablate >= 10 && ablate <= 12);
+    const bool full = ablate == 0 || ablate == 20 || ablate == 31 || ablate == 40 || (ablate >= 10 && ablate <= 12);
     const bool keep_rows = !force_scan && n_sets == 1 && full;
     w->rows_rs = keep_rows ? sets[0] : nullptr;
     w->rows_n = n;
@@ -399,7 +419,13 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
             perm = w->d_perm;
         }
         w->rows_perm = perm;
-        if (lane) {
+        if (row) {
+            w->rows_perm = nullptr;  // (one row per request)
+            w->rows_wave = false;
+            HIP_OK(ajx::launch_eval_row(w->d_sets, (uint32_t)sets[0]->c.blob.size(), h0->n_selectors, d_arena, d_offs,
+                                        d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
+                                        w->d_rows, row_stride, w->d_slow, w->d_tier, s, perm, mods, ablate));
+        } else if (lane) {
             const uint32_t stage_bytes =
                 n_sets == 1 && max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u;
             HIP_OK(ajx::launch_eval_lane(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,

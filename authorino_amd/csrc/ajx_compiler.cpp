@@ -658,6 +658,7 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
 
     // ---- assemble ----
     Builder b;
+    uint32_t hdr_row_off = 0;
     RulesetHdr hdr;
     std::memset(&hdr, 0, sizeof hdr);
     b.append(&hdr, sizeof hdr);
@@ -720,6 +721,86 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         b.append(tc.data(), tc.size() * sizeof(TrieChild));
         hdr.off_key_slots = (uint32_t)b.align16();
         b.append(slots.data(), slots.size() * sizeof(KeySlot));
+        // row kernel tables: key ids, transition table, key dictionary, index edges
+        // (kept before hot_bytes: every table a single-pass kernel reads)
+        if (fast_ok) {
+            std::map<std::string, uint32_t> kid_of;
+            std::vector<std::string> kid_keys;
+            bool row_ok = true;
+            std::vector<uint32_t> idx_edges;
+            for (size_t i = 0; i < trie.size(); i++)
+                for (size_t j = 0; j < trie[i].kids.size(); j++) {
+                    const std::string& key = trie[i].keys[j].first;
+                    if (!kid_of.count(key)) {
+                        kid_of[key] = (uint32_t)kid_keys.size();
+                        kid_keys.push_back(key);
+                    }
+                    const int32_t ai = trie[i].keys[j].second;
+                    if (ai >= 0) {
+                        if (ai > 0xFFFF) row_ok = false;
+                        idx_edges.push_back((uint32_t)i | (trie[i].kids[j] << 8) | ((uint32_t)ai << 16));
+                    }
+                    if (key.size() > 0xFFFF) row_ok = false;
+                }
+            if (kid_keys.size() > kRowMaxKids) row_ok = false;
+            const uint32_t nk = (uint32_t)std::max<size_t>(kid_keys.size(), 1);
+            if ((uint64_t)trie.size() * nk > 64 * 1024) row_ok = false;
+            // dictionary: load <= 1/2, grown until every key is within kRowDictProbes of home
+            uint32_t dlog2 = 2, dprobes = 1;
+            std::vector<KeyDictSlot> dict;
+            std::vector<uint32_t> key_off(kid_keys.size());
+            for (size_t k = 0; k < kid_keys.size(); k++) {
+                while (lits.size() % 4) lits.push_back('\0');
+                key_off[k] = (uint32_t)lits.size();
+                lits += kid_keys[k];
+            }
+            while (row_ok) {
+                while ((1u << dlog2) < 2 * kid_keys.size()) dlog2++;
+                dict.assign(1u << dlog2, KeyDictSlot{0, 0, 0xFFFFFFFFu, 0});
+                dprobes = 1;
+                for (size_t k = 0; k < kid_keys.size(); k++) {
+                    const std::string& key = kid_keys[k];
+                    const uint64_t sig = key_signature((const uint8_t*)key.data(), (uint32_t)key.size());
+                    uint32_t at = kdict_slot(sig, (uint32_t)key.size(), dlog2), dist = 1;
+                    while (dict[at].meta != 0xFFFFFFFFu) at = (at + 1) & ((1u << dlog2) - 1), dist++;
+                    dict[at] = KeyDictSlot{(uint32_t)sig, (uint32_t)(sig >> 32),
+                                           (uint32_t)key.size() | ((uint32_t)k << 16), key_off[k]};
+                    dprobes = std::max(dprobes, dist);
+                }
+                if (dprobes <= kRowDictProbes) break;
+                if (dlog2 >= kRowMaxDictLog2) { row_ok = false; break; }
+                dlog2++;
+            }
+            if (row_ok) {
+                std::vector<uint32_t> nodes(trie.size(), 0);
+                std::vector<uint8_t> trans(trie.size() * nk, 0xFF);
+                for (size_t i = 0; i < trie.size(); i++) {
+                    nodes[i] = trie[i].selector >= 0 ? (uint32_t)trie[i].selector + 1u : 0u;
+                    for (size_t j = 0; j < trie[i].kids.size(); j++) {
+                        trans[i * nk + kid_of[trie[i].keys[j].first]] = (uint8_t)trie[i].kids[j];
+                        if (trie[i].keys[j].second >= 0) nodes[i] |= 1u << 8;
+                    }
+                }
+                RowHdr rh;
+                std::memset(&rh, 0, sizeof rh);
+                hdr_row_off = (uint32_t)b.align16();
+                b.append(&rh, sizeof rh);
+                rh.off_nodes = (uint32_t)b.align16();
+                b.append(nodes.data(), nodes.size() * 4);
+                rh.n_nodes = (uint32_t)nodes.size();
+                rh.off_trans = (uint32_t)b.align16();
+                b.append(trans.data(), trans.size());
+                rh.n_kids = (uint32_t)kid_keys.size();
+                rh.off_kdict = (uint32_t)b.align16();
+                b.append(dict.data(), dict.size() * sizeof(KeyDictSlot));
+                rh.kd_log2 = dlog2;
+                rh.kd_probes = dprobes;
+                rh.off_idx = (uint32_t)b.align16();
+                b.append(idx_edges.data(), idx_edges.size() * 4);
+                rh.n_idx = (uint32_t)idx_edges.size();
+                std::memcpy(b.blob.data() + hdr_row_off, &rh, sizeof rh);
+            }
+        }
         std::vector<SelectorPatterns> sp(sels.size());
         std::vector<uint16_t> plist;
         for (size_t s = 0; s < sels.size(); s++) {
@@ -798,6 +879,7 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     hdr.lit_bytes = (uint32_t)lits.size();
     hdr.n_components = (uint32_t)comps.size();
     hdr.flags = flags;
+    hdr.off_row = hdr_row_off;
     std::memcpy(b.blob.data(), &hdr, sizeof hdr);
     out->blob = std::move(b.blob);
     out->n_patterns = np;

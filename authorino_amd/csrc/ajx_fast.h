@@ -743,6 +743,28 @@ AJX_HD uint32_t load_u32_upto(const uint8_t* p, uint32_t avail) {
 #endif
 }
 
+// A JSON number that is its own FormatFloat(f, 'f', -1, 64) (gjson Result.String() of a
+// non-integer Number): (0|[1-9][0-9]*)\.[0-9]*[1-9] with at most 15 digits in all — a
+// decimal of <= 15 significant digits is the only such decimal that parses to its double,
+// so the shortest round-trip digits are its own (the sign is handled by the caller).
+AJX_HD bool simple_decimal(const uint8_t* s, uint32_t n) {
+    if (n < 3 || n > 16) return false;
+    uint32_t i = 0, nd = 0;
+    if (s[0] == '0') {
+        i = 1;
+        nd = 1;
+    } else {
+        while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+        nd = i;
+        if (i == 0) return false;
+    }
+    if (i >= n || s[i] != '.') return false;
+    const uint32_t f0 = ++i;
+    while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+    if (i != n || i == f0 || s[n - 1] == '0') return false;
+    return nd + (n - f0) <= 15;
+}
+
 struct RawVal {
     uint32_t a, n;  // span in the document
     uint32_t lit;   // 0 span, kLitTrue / kLitFalse / kLitEmpty for the literals
@@ -759,12 +781,14 @@ AJX_HD RawVal raw_value(const uint8_t* doc, const ValueRef& v) {
         case T_NUMBER: {
             uint32_t k = v.start;
             if (k < v.end && doc[k] == '-') k++;
+            const uint32_t k0 = k;
             for (; k < v.end; k += 4) {  // -?[0-9]* is its own String()
                 const uint32_t w = load_u32_upto(doc + k, v.end - k);
                 const uint32_t m = v.end - k >= 4 ? 0xFFFFFFFFu : (1u << (8 * (v.end - k))) - 1u;
                 const uint32_t d = w ^ 0x30303030u;
                 if ((((d + 0x76767676u) | d) & 0x80808080u) & m) { r.ok = false; break; }
             }
+            if (!r.ok) r.ok = simple_decimal(doc + k0, v.end - k0);
             break;
         }
         case T_TRUE: r.lit = kLitTrue; r.n = 4; break;
@@ -841,6 +865,143 @@ AJX_HD bool dfa_match_lit(const uint8_t* blob, uint32_t dfa_off, uint32_t lit) {
     const uint32_t n = lit == kLitTrue ? 4u : lit == kLitFalse ? 5u : 0u;
     for (uint32_t k = 0; k < n; k++) {
         st = tr[st * nc + h->ascii_class[(text >> (8 * k)) & 0x7Fu]];
+        if (st == ms) return true;
+    }
+    return blob[h->eot_off + st] != 0;
+}
+
+// The gjson unescape of a string's contents as a byte stream (StrSrc::S_UNESC) with
+// every byte of state in registers: the UTF-8 bytes of a \u escape wait packed in `pend`.
+struct UnescSrc {
+    const uint8_t* p;
+    uint32_t i, n;
+    uint32_t pend, npend;
+    bool done;
+    AJX_HD void init(const uint8_t* s, uint32_t a, uint32_t b) {
+        p = s;
+        i = a;
+        n = b;
+        pend = npend = 0;
+        done = false;
+    }
+    AJX_HD int next() {
+        if (npend) {
+            const int c = (int)(pend & 0xFFu);
+            pend >>= 8;
+            npend--;
+            return c;
+        }
+        if (done || i >= n) return -1;
+        const uint8_t c = p[i];
+        if (c < ' ') { done = true; return -1; }
+        if (c != '\\') { i++; return c; }
+        i++;
+        if (i >= n) { done = true; return -1; }
+        const uint8_t e = p[i];
+        uint8_t out;
+        switch (e) {
+            case '\\': out = '\\'; break;
+            case '/': out = '/'; break;
+            case 'b': out = '\b'; break;
+            case 'f': out = '\f'; break;
+            case 'n': out = '\n'; break;
+            case 'r': out = '\r'; break;
+            case 't': out = '\t'; break;
+            case '"': out = '"'; break;
+            case 'u': {
+                if (i + 5 > n) { done = true; return -1; }
+                uint32_t r = hexval4(p + i + 1);
+                i += 5;
+                if (r >= 0xD800 && r < 0xE000) {
+                    if (n - i >= 6 && p[i] == '\\' && p[i + 1] == 'u') {
+                        const uint32_t r2 = hexval4(p + i + 2);
+                        if (r < 0xDC00 && r2 >= 0xDC00 && r2 < 0xE000)
+                            r = (((r - 0xD800) << 10) | (r2 - 0xDC00)) + 0x10000;
+                        else
+                            r = 0xFFFD;
+                        i += 6;
+                    }
+                }
+                // utf8_put, packed low byte first
+                if (r > 0x10FFFF || (r >= 0xD800 && r <= 0xDFFF)) r = 0xFFFD;
+                uint32_t b;
+                uint32_t k;
+                if (r < 0x80) { b = r; k = 1; }
+                else if (r < 0x800) { b = (0xC0 | (r >> 6)) | ((0x80 | (r & 0x3F)) << 8); k = 2; }
+                else if (r < 0x10000) {
+                    b = (0xE0 | (r >> 12)) | ((0x80 | ((r >> 6) & 0x3F)) << 8) | ((0x80 | (r & 0x3F)) << 16);
+                    k = 3;
+                } else {
+                    b = (0xF0 | (r >> 18)) | ((0x80 | ((r >> 12) & 0x3F)) << 8) | ((0x80 | ((r >> 6) & 0x3F)) << 16) |
+                        ((0x80 | (r & 0x3F)) << 24);
+                    k = 4;
+                }
+                pend = b >> 8;
+                npend = k - 1;
+                return (int)(b & 0xFFu);
+            }
+            default: done = true; return -1;
+        }
+        i++;
+        return out;
+    }
+};
+
+// stream == literal (UnescSrc)
+AJX_HD bool unesc_equals(UnescSrc* s, const uint8_t* lit, uint32_t len) {
+    for (uint32_t k = 0; k < len; k++)
+        if (s->next() != (int)lit[k]) return false;
+    return s->next() < 0;
+}
+
+// `matches` over a UnescSrc: utf8.DecodeRune over the stream with the (up to 4) bytes
+// of lookahead packed in a register (RuneReader, without its arrays)
+AJX_HD bool dfa_match_unesc(const uint8_t* blob, uint32_t dfa_off, UnescSrc* s) {
+    const DfaHdr* h = (const DfaHdr*)(blob + dfa_off);
+    const uint16_t* tr = (const uint16_t*)(blob + h->trans_off);
+    const uint32_t nc = h->n_classes, ms = h->match_state;
+    uint32_t st = h->start;
+    if (st == ms) return true;
+    uint32_t la = 0, nla = 0;
+    for (;;) {
+        while (nla < 4) {
+            const int c = s->next();
+            if (c < 0) break;
+            la |= (uint32_t)c << (8 * nla);
+            nla++;
+        }
+        if (nla == 0) break;
+        const uint32_t b0 = la & 0xFFu;
+        uint32_t sz = 1;
+        int32_t r = (int32_t)b0;
+        if (b0 >= 0x80) {
+            r = 0xFFFD;
+            uint32_t need = 0, lo = 0x80, hi = 0xBF, v = 0;
+            if (b0 >= 0xC2 && b0 <= 0xDF) { need = 2; v = b0 & 0x1F; }
+            else if (b0 >= 0xE0 && b0 <= 0xEF) {
+                need = 3; v = b0 & 0x0F;
+                if (b0 == 0xE0) lo = 0xA0;
+                if (b0 == 0xED) hi = 0x9F;
+            } else if (b0 >= 0xF0 && b0 <= 0xF4) {
+                need = 4; v = b0 & 0x07;
+                if (b0 == 0xF0) lo = 0x90;
+                if (b0 == 0xF4) hi = 0x8F;
+            }
+            const uint32_t b1 = (la >> 8) & 0xFFu;
+            if (need && nla >= need && b1 >= lo && b1 <= hi) {
+                bool good = true;
+                v = (v << 6) | (b1 & 0x3Fu);
+                for (uint32_t k = 2; k < need; k++) {
+                    const uint32_t c = (la >> (8 * k)) & 0xFFu;
+                    if (c < 0x80 || c > 0xBF) { good = false; break; }
+                    v = (v << 6) | (c & 0x3Fu);
+                }
+                if (good) { r = (int32_t)v; sz = need; }
+            }
+        }
+        la = sz == 4 ? 0u : la >> (8 * sz);
+        nla -= sz;
+        st = tr[st * nc + rune_class(h, blob, r)];
         if (st == ms) return true;
     }
     return blob[h->eot_off + st] != 0;

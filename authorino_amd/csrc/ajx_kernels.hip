@@ -668,6 +668,33 @@ hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_
 }
 
 // ---------------------------------------------------------------------------------
+// The row kernel (ajx_row.h): four documents per wavefront, 16 lanes each. Workgroups
+// of 4 waves stage the ruleset blob in LDS next to each wave's row buffers, then every
+// wave walks groups of four requests (grid-stride; the requests of a group are
+// consecutive in the length-bucketed order, so their lengths are alike). A tier takes
+// the documents that fit its row buffers (maxb); longer ones go to the next tier's list
+// (the last tier's "next" is the exact scan's list), as do the ones the row scan can not
+// prove. Output: each request's capture row (row r, header kRowSlow when handed over).
+// ---------------------------------------------------------------------------------
+hipError_t launch_eval_row(const uint8_t* const* d_sets, uint32_t blob_bytes, uint32_t n_selectors,
+                           const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                           uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
+                           uint32_t row_stride, uint32_t* d_slow, uint32_t* d_tier, hipStream_t stream,
+                           const uint32_t* d_perm, bool mods, int mode) {
+    if (n == 0) return hipSuccess;
+    if ((d_rows && row_stride < 1 + n_selectors) || n_selectors > 64u) return hipErrorInvalidValue;
+    hipError_t e = launch_row_scan(d_sets, blob_bytes, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_tri, d_err,
+                                   d_bm, stride, d_slow, d_tier, stream, d_perm);
+    if (e != hipSuccess) return e;
+    if (mode == 41) return hipSuccess;  // profiling: the row kernel alone
+    const uint32_t grid = (n + 255u) / 256u;
+    const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
+    launch_slow_list(mods, sgrid, stream, d_sets, nullptr, d_arena, d_offs, d_lens, d_slow, d_slow + 1, d_tri, d_err,
+                     d_bm, stride);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
 // Length bucketing: a wave of the single-pass kernel runs each window's token loop as
 // long as its busiest lane, and the whole document loop as long as its longest
 // document, so the 64 requests of a wave should have similar lengths. A counting sort

@@ -53,8 +53,21 @@ EXPORTS = [
     "authjx_ruleset_trees", "authjx_batcher_create", "authjx_batcher_destroy", "authjx_batcher_eval",
     "authjx_batcher_stats",
     "authjx_index_new", "authjx_index_free", "authjx_index_set", "authjx_index_delete_key", "authjx_index_get",
-    "authjx_index_lookup_batch", "authjx_pack_json",
+    "authjx_index_lookup_batch", "authjx_pack_json", "authjx_build_hash",
 ]
+
+
+def _check_build_hash(L, path: str) -> None:
+    """The binary must have been built from the sources next to it (when they are here)."""
+    from . import build as _b
+
+    if not os.path.isdir(_b.CSRC):
+        return
+    want = _b.source_hash()
+    got = (L.authjx_build_hash() or b"").decode()
+    if got != want:
+        raise AuthjxError(f"{path} was built from other sources (hash {got}, sources {want}): "
+                          "run __graft_entry__.build()")
 
 
 def load_library(path: str = LIB_PATH):
@@ -73,6 +86,9 @@ def load_library(path: str = LIB_PATH):
         except ImportError:
             pass
         L = C.CDLL(path)
+        L.authjx_build_hash.argtypes = []
+        L.authjx_build_hash.restype = C.c_char_p
+        _check_build_hash(L, path)
         L.authjx_init.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         L.authjx_init.restype = C.c_int
         L.authjx_shutdown.argtypes = [C.c_void_p]

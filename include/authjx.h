@@ -128,6 +128,9 @@ typedef struct {
 /* Device context: one per GPU (device ordinal). */
 int authjx_init(int device, authjx_ctx** out);
 void authjx_shutdown(authjx_ctx* ctx);
+// The sha256 (first 32 hex digits) of the sources the library was built from
+// (authorino_amd/build.py source_hash); the Python runtime refuses a stale binary.
+const char* authjx_build_hash(void);
 int authjx_device_count(void);
 
 /* Compile one tree into a device-resident ruleset. pattern_status (n_patterns entries,

@@ -219,3 +219,45 @@ class LaneRuleset:
     def __del__(self):
         if getattr(self, "_h", None):
             lane_lib().hw_free(self._h)
+
+
+def _row_decl():
+    L = lib()
+    if not hasattr(L, "_row_declared"):
+        L.rt_scan.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                              C.c_uint32, C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32]
+        L.rt_scan.restype = C.c_int
+        L.rt_eval.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8),
+                              C.POINTER(C.c_int32), C.c_uint32, C.c_uint32]
+        L.rt_eval.restype = C.c_int
+        L._row_declared = True
+    return L
+
+
+ROW_MAXB, ROW_MAXE = 8192, 2048
+
+
+def eval_row(hr: "HostRuleset", doc, mis: int = 0, maxb: int = ROW_MAXB, maxe: int = ROW_MAXE):
+    """The row kernel (64-lane host emulation) + stage B: (tri | -1 exact scan | -2 no row
+    tables, err, res)."""
+    L = _row_decl()
+    d = _b(doc)
+    res = (C.c_uint8 * max(hr.n, 1))()
+    err = C.c_int32(-1)
+    t = L.rt_eval(hr._h, d, len(d), mis, res, C.byref(err), maxb, maxe)
+    return t, err.value, list(res)[: hr.n]
+
+
+def scan_rows(hr: "HostRuleset", docs, mis, n_sel: int, maxb: int = ROW_MAXB, maxe: int = ROW_MAXE):
+    """Up to four documents as one wavefront of the row kernel: their capture rows
+    (header kRowSlow = exact scan)."""
+    L = _row_decl()
+    nd = len(docs)
+    bs = [_b(x) for x in docs]
+    arr = (C.c_char_p * 4)(*(bs + [b""] * (4 - nd)))
+    lens = (C.c_uint32 * 4)(*([len(x) for x in bs] + [0] * (4 - nd)))
+    ms = (C.c_uint32 * 4)(*(list(mis) + [0] * (4 - nd)))
+    rows = (C.c_uint64 * (4 * (1 + n_sel)))()
+    rc = L.rt_scan(hr._h, arr, lens, ms, nd, rows, maxb, maxe)
+    out = list(rows)
+    return rc, [out[k * (1 + n_sel):(k + 1) * (1 + n_sel)] for k in range(nd)]

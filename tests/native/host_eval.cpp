@@ -227,3 +227,152 @@ static int eval_single_pass(void* h, const uint8_t* doc, uint32_t len, uint32_t 
 }
 
 extern "C" uint32_t ht_blob_size(void* h) { return (uint32_t)((HtRuleset*)h)->c.blob.size(); }
+
+// ---------------------------------------------------------------------------------
+// The row kernel (ajx_row.h) on the 64-lane host emulation (ajx_wave.h): up to four
+// documents as one wavefront's rows. rows_out: 4 x (1 + n_selectors) capture rows
+// (header kRowSlow when the document goes to the exact scan). Returns the number of
+// rows accepted, or -2 when the ruleset has no row tables.
+#include "../../authorino_amd/csrc/ajx_row.h"
+extern "C" int rt_scan(void* h, const uint8_t* const* docs, const uint32_t* lens, const uint32_t* mis_in, uint32_t nd,
+                       uint64_t* rows_out, uint32_t maxb, uint32_t maxe) {
+    using namespace ajx::w;
+    std::vector<uint8_t> blobv = ((HtRuleset*)h)->c.blob;
+    const uint8_t* gblob = blobv.data();
+    const RulesetHdr* hd = (const RulesetHdr*)gblob;
+    if (!(hd->flags & kFlagFastOk) || hd->off_row == 0) return -2;
+    const RowLayout L = row_layout(maxb, maxe);
+    std::vector<uint8_t> lds(L.bytes + 64, 0xA5);
+    const RowTabs T = row_tabs(gblob, blobv.data());
+    // each document in its own buffer at the requested misalignment (slack around it)
+    std::vector<std::vector<uint8_t>> bufs(4);
+    const uint8_t* bases[4] = {nullptr, nullptr, nullptr, nullptr};
+    V len(0u), mis(0u);
+    M live(false);
+    for (uint32_t r = 0; r < 4; r++) {
+        bufs[r].assign((r < nd ? lens[r] : 0) + 64, 0x5A);
+        uintptr_t a = ((uintptr_t)bufs[r].data() + 15) & ~(uintptr_t)15;
+        const uint32_t m = r < nd ? (mis_in[r] & 15u) : 0u;
+        if (r < nd && lens[r]) std::memcpy((uint8_t*)a + m, docs[r], lens[r]);
+        bases[r] = (const uint8_t*)a;
+        for (int l = 0; l < 16; l++) {
+            len.x[16 * r + l] = r < nd ? lens[r] : 0u;
+            mis.x[16 * r + l] = m;
+            if (r < nd) live.b |= 1ull << (16 * r + l);
+        }
+    }
+    auto load = [&](const V& b, const M& m) -> G16 {
+        P a;
+        for (int l = 0; l < 64; l++) a.p[l] = m.at(l) ? bases[l >> 4] + 16u * b.x[l] : nullptr;
+        return gld128(a, m);
+    };
+    const uint32_t ns = hd->n_selectors;
+    M ok = row_scan(T, lds.data(), L, live, len, mis, load);
+    std::vector<uint64_t> recs(4 * (size_t)(1 + ns), 0);
+    V hlo, hhi;
+    ok = row_finish(T, lds.data(), L, ok, mis, hlo, hhi,
+                    [&](const V& s, const M& m, const M& found, const V& start, const V& ln, const V& type, const V& esc) {
+                        for (int l = 0; l < 64; l++) {
+                            if (!m.at(l)) continue;
+                            const uint32_t r = l >> 4;
+                            const uint64_t rec = found.at(l) ? ((uint64_t)start.x[l] |
+                                                                ((uint64_t)((ln.x[l] & 0xFFFFFFu) | (type.x[l] << 24) |
+                                                                            (esc.x[l] << 27)) << 32))
+                                                             : 0ull;
+                            if (found.at(l)) recs[r * (1 + ns) + 1 + s.x[l]] = rec;
+                        }
+                    });
+    int acc = 0;
+    for (uint32_t r = 0; r < nd; r++) {
+        uint64_t* ro = rows_out + (size_t)r * (1 + ns);
+        if (!ok.at(16 * r)) {
+            ro[0] = kRowSlow;
+            continue;
+        }
+        acc++;
+        ro[0] = (uint64_t)hlo.x[16 * r] | ((uint64_t)hhi.x[16 * r] << 32);
+        for (uint32_t s = 0; s < ns; s++) ro[1 + s] = recs[r * (1 + ns) + 1 + s];
+    }
+    return acc;
+}
+
+// the whole row kernel (row scan + in-kernel stage B) for up to four documents:
+// tri[d * n_trees + k], err[...], bm[d * bm_words + w]; returns a bit per document that
+// stayed on the row path (the others belong to the exact scan).
+extern "C" int rt_run(void* h, const uint8_t* const* docs, const uint32_t* lens, const uint32_t* mis_in, uint32_t nd,
+                      uint8_t* tri, int32_t* err, uint64_t* bm, uint32_t bm_words, uint32_t maxb, uint32_t maxe) {
+    using namespace ajx::w;
+    std::vector<uint8_t> blobv = ((HtRuleset*)h)->c.blob;
+    const uint8_t* gblob = blobv.data();
+    const RulesetHdr* hd = (const RulesetHdr*)gblob;
+    if (!(hd->flags & kFlagFastOk) || hd->off_row == 0) return -2;
+    const RowLayout L = row_layout(maxb, maxe);
+    std::vector<uint8_t> lds(L.bytes + 64, 0xA5);
+    const RowTabs T = row_tabs(gblob, blobv.data());
+    std::vector<std::vector<uint8_t>> bufs(4);
+    const uint8_t* bases[4] = {nullptr, nullptr, nullptr, nullptr};
+    V len(0u), mis(0u), r(0u);
+    M live(false);
+    for (uint32_t d = 0; d < 4; d++) {
+        bufs[d].assign((d < nd ? lens[d] : 0) + 64, 0x5A);
+        uintptr_t a = ((uintptr_t)bufs[d].data() + 15) & ~(uintptr_t)15;
+        const uint32_t m = d < nd ? (mis_in[d] & 15u) : 0u;
+        if (d < nd && lens[d]) std::memcpy((uint8_t*)a + m, docs[d], lens[d]);
+        bases[d] = (const uint8_t*)a;
+        for (int l = 0; l < 16; l++) {
+            len.x[16 * d + l] = d < nd ? lens[d] : 0u;
+            mis.x[16 * d + l] = m;
+            r.x[16 * d + l] = d;
+            if (d < nd) live.b |= 1ull << (16 * d + l);
+        }
+    }
+    auto load = [&](const V& b, const M& m) -> G16 {
+        P a;
+        for (int l = 0; l < 64; l++) a.p[l] = m.at(l) ? bases[l >> 4] + 16u * b.x[l] : nullptr;
+        return gld128(a, m);
+    };
+    M ok = row_scan(T, lds.data(), L, live, len, mis, load);
+    V hlo, hhi;
+    ok = row_finish(T, lds.data(), L, ok, mis, hlo, hhi,
+                    [&](const V&, const M&, const M&, const V&, const V&, const V&, const V&) {});
+    const uint32_t nt = hd->pad1[0] ? hd->pad1[0] : 1u;
+    ok = row_patterns(
+        gblob, lds.data(), L, ok, mis, r,
+        [&](uint32_t d, uint32_t k, uint32_t ntr, uint8_t t, int32_t e) {
+            tri[d * ntr + k] = t;
+            if (err) err[d * ntr + k] = e;
+        },
+        [&](uint32_t d, uint32_t k, uint64_t word) {
+            if (bm) bm[(size_t)d * bm_words + k] = word;
+        },
+        bm ? bm_words : 0u);
+    (void)nt;
+    int acc = 0;
+    for (uint32_t d = 0; d < nd; d++)
+        if (ok.at(16 * d)) acc |= 1 << d;
+    return acc;
+}
+
+// the row kernel for one document: -1 exact scan, -2 no row tables, else the tri-state
+// of the (first) tree; res[p] per pattern from the bitmap (and the static errors / the
+// undecided-by-design patterns as the fold sees them)
+extern "C" int rt_eval(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
+                       uint32_t maxb, uint32_t maxe) {
+    const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
+    const RulesetHdr* hd = (const RulesetHdr*)blob;
+    const uint32_t nt = hd->pad1[0] ? hd->pad1[0] : 1u;
+    std::vector<uint8_t> tri(nt);
+    std::vector<int32_t> errs(nt);
+    uint64_t bm[2] = {0, 0};
+    const uint8_t* docs[1] = {doc};
+    const int rc = rt_run(h, docs, &len, &mis, 1, tri.data(), errs.data(), bm, 2, maxb, maxe);
+    if (rc < 0) return rc;
+    if (!(rc & 1)) return -1;
+    for (uint32_t p = 0; p < hd->n_patterns; p++) {
+        uint64_t bit = 1ull << (p & 63);
+        uint32_t k = p >> 6;
+        res[p] = (hd->static_error[k] & bit) ? V_E : (hd->unsupported[k] & bit) ? V_U : (bm[k] & bit) ? V_T : V_F;
+    }
+    if (err) *err = errs[0];
+    return tri[0];
+}
