@@ -80,9 +80,9 @@ struct authjx_ctx {
     int len_sort = 1;         // order requests by length class before the single-pass kernel
     int no_tenant_stage = 0;  // profiling: multi-tenant batches read tables from global memory
     int force_scan = 0;
-    int ablate = 0;  // profiling only: 1/2/3 reduced single-pass variants, 20 the lane kernel,
-                     // 21..24 its ablations (ajx_kernels.hip ajx_lane_eval), 31 the
-                     // single-pass kernel with the event scanner (ajx_events.h) for stage A
+    int ablate = 0;  // profiling only: 40 the token-scanner single-pass kernel, 41 the row
+                     // kernel without the exact scan after it, 1..3 / 10..12 token-scanner
+                     // ablations and workgroup sizes
 };
 
 namespace {
@@ -380,14 +380,12 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         if (rc != AUTHJX_OK) return rc;
     }
     HIP_OK(hipEventRecord(w->ev0, s));
-    // kernel: the single-pass kernel (default; ajx_scan_fused with the token scanner);
-    // ablate 31 the same kernel with the event scanner, 20 the lane kernel (21..24 its
-    // ablations), 1..3 single-pass ablations, 10..12 the single-pass kernel in 4-, 8- or
-    // 16-wave workgroups
+    // kernel: the row kernel (default for a batch over one ruleset, ajx_row.h); the
+    // token-scanner single-pass kernel (ajx_scan_fused) for multi-tenant batches and on
+    // ablate 40; 1..3 / 10..12 its profiling variants
     bool fast_tables = !force_scan;
     for (uint32_t i = 0; i < n_sets && fast_tables; i++)
         fast_tables = (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagFastOk) != 0;
-    const bool lane = fast_tables && ablate >= 20 && ablate < 30;
     bool mods = false;  // modifier chains: the exact scan's instance with text buffers
     for (uint32_t i = 0; i < n_sets; i++)
         mods = mods || reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->n_modifiers != 0 ||
@@ -395,16 +393,17 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     // the row kernel (ajx_row.h; default for a batch over one ruleset with row tables);
     // ablate 40 keeps the token-scanner single-pass kernel, 41 is the row scan alone
     const ajx::RulesetHdr* h0 = reinterpret_cast<const ajx::RulesetHdr*>(sets[0]->c.blob.data());
-    const bool row = fast_tables && n_sets == 1 && (ablate == 0 || ablate == 41) && h0->off_row != 0 &&
-                     h0->n_selectors <= 64 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes;
+    const bool row = fast_tables && n_sets == 1 && (ablate == 0 || (ablate >= 41 && ablate <= 44)) && h0->off_row != 0 &&
+                     h0->n_selectors <= 64 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes &&
+                     ajx::row_kernel_fits((uint32_t)sets[0]->c.blob.size());
     // capture rows kept for authjx_select_from_eval_device: one ruleset, a full kernel
-    const bool full = ablate == 0 || ablate == 20 || ablate == 31 || ablate == 40 || (ablate >= 10 && ablate <= 12);
+    const bool full = ablate == 0 || ablate == 40 || (ablate >= 10 && ablate <= 12);
     const bool keep_rows = !force_scan && n_sets == 1 && full;
     w->rows_rs = keep_rows ? sets[0] : nullptr;
     w->rows_n = n;
     w->rows_stride = row_stride;
     w->rows_perm = nullptr;
-    w->rows_wave = !lane;  // (the lane kernel keeps one row per request)
+    w->rows_wave = true;
     size_t max_blob = 0;
     for (uint32_t i = 0; i < n_sets; i++) max_blob = std::max(max_blob, sets[i]->c.blob.size());
     if (force_scan) {
@@ -420,18 +419,16 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         }
         w->rows_perm = perm;
         if (row) {
-            w->rows_perm = nullptr;  // (one row per request)
+            // the row kernel decides in-kernel; it writes capture rows (one per request)
+            // only for a forest, whose selector tree authjx_select_from_eval_device reads
+            const bool rows = keep_rows && sets[0]->c.n_trees > 1;
+            if (!rows) w->rows_rs = nullptr;
+            w->rows_perm = nullptr;
             w->rows_wave = false;
             HIP_OK(ajx::launch_eval_row(w->d_sets, (uint32_t)sets[0]->c.blob.size(), h0->n_selectors, d_arena, d_offs,
                                         d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
-                                        w->d_rows, row_stride, w->d_slow, w->d_tier, s, perm, mods, ablate));
-        } else if (lane) {
-            const uint32_t stage_bytes =
-                n_sets == 1 && max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u;
-            HIP_OK(ajx::launch_eval_lane(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
-                                         d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
-                                         w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s, ablate - 20, perm,
-                                         mods));
+                                        rows ? w->d_rows : nullptr, row_stride, w->d_slow, w->d_tier, s, perm, mods,
+                                        ablate));
         } else {
             // uniform batch: the blob staged once per workgroup; multi-tenant batch: nonzero
             // turns on the per-workgroup staging of its runs' rulesets (ajx_scan_fused_tenant)
@@ -441,7 +438,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
             HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                          d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
                                          w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
-                                         ablate < 20 || ablate == 31 ? ablate : 0, perm, mods));
+                                         ablate < 20 ? ablate : 0, perm, mods));
         }
     }
     return batch_done(w, sets, n_sets);

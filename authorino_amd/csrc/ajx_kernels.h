@@ -51,19 +51,6 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
                             int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false);
 
-// The lane kernel (ajx_lane.h): one work-item per request over 64-byte windows the
-// wavefront stages through LDS with coalesced loads; stage B in the same work-item;
-// requests it can not prove valid compact JSON go to the exact scan (launched after it).
-// d_rows: capture rows (row_stride u64 per request, kept for authjx_select_from_eval).
-// d_perm (may be null): length-bucketed request order. mode (profiling, uniform ruleset
-// only, outputs meaningless): 1 the window staging alone, 2 no token walk and no stage B,
-// 3 no key lookups, 4 no stage B.
-hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
-                            const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
-                            uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
-                            uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false);
-
 // The row kernel (ajx_row.h, one ruleset for the whole batch, blob with row tables):
 // capture rows for every request (d_rows, row_stride u64 each, one per request), then
 // stage B, then the exact scan of what it handed over. d_slow: [0] count + n ids;
@@ -74,12 +61,16 @@ hipError_t launch_eval_row(const uint8_t* const* d_sets, uint32_t blob_bytes, ui
                            uint32_t row_stride, uint32_t* d_slow, uint32_t* d_tier, hipStream_t stream,
                            const uint32_t* d_perm, bool mods, int mode);
 
+// The row kernel's LDS (ruleset blob + every tier's row buffers) fits a workgroup.
+bool row_kernel_fits(uint32_t blob_bytes);
+
 // The row kernel (ajx_rowk.hip): the tiers' launches, stage B included; d_rows (may be
 // null) receives the capture rows.
 hipError_t launch_row_scan(const uint8_t* const* d_sets, uint32_t blob_bytes, const uint8_t* d_arena,
                            const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint64_t* d_rows,
                            uint32_t row_stride, uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride,
-                           uint32_t* d_slow, uint32_t* d_tier, hipStream_t stream, const uint32_t* d_perm);
+                           uint32_t* d_slow, uint32_t* d_tier, hipStream_t stream, const uint32_t* d_perm,
+                           uint32_t stop = 0);
 
 // Length-bucketed request order for the single-pass kernel: d_perm[n] = request ids,
 // longest 8-byte length class first; d_hist needs 2 * 1024 + 1 u32 of scratch.

@@ -6,8 +6,6 @@
 //                Requests it can not prove gjson-equivalent go to a slow list.
 // ajx_patterns   stage B, one work-item per request: patterns on the captured values,
 //                T bitmap, And/Or fold.
-// ajx_lane_eval  the lane kernel (ajx_lane.h): work-item per request over 64-byte
-//                windows the wavefront stages through LDS with coalesced loads
 // ajx_eval_scan  one work-item per request on the slow list (or on every request when
 //                forced): for each selector an exact gjson.Get scan (ajx_device.h gj_get),
 //                then the patterns and the fold. Exact for arbitrary input bytes.
@@ -15,9 +13,7 @@
 
 #include <atomic>
 
-#include "ajx_events.h"
 #include "ajx_fast.h"
-#include "ajx_lane.h"
 #include "ajx_modifiers.h"
 #include "ajx_kernels.h"
 
@@ -240,8 +236,7 @@ __device__ __forceinline__ WinRing lane_ring(uint32_t ring_off) {
 }
 
 // stage A for request r: single-pass scan into its capture row (false: slow list)
-// EV: the event scanner (ajx_events.h); otherwise ajx_fast.h's token scanner (the default)
-template <int MODE, bool EV = false>
+template <int MODE>
 __device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t* d, uint32_t len, RowRef row,
                                              const WinRing& ring) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
@@ -257,8 +252,7 @@ __device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t*
         }
         return Block16{0u, 0u, 0u, 0u};
     };
-    if constexpr (EV) return scan_doc_ev(blob, blob_tables(blob), d, len, row, ring, load);
-    else return scan_doc<MODE>(blob, blob_tables(blob), d, len, row, ring, load);
+    return scan_doc<MODE>(blob, blob_tables(blob), d, len, row, ring, load);
 }
 
 // the And/Or fold of every tree of the ruleset on the pattern bitmaps; a forest ruleset
@@ -343,7 +337,7 @@ __global__ __launch_bounds__(kFastMaxBlock) void ajx_patterns(const uint8_t* con
 // The single-pass path: stage A then stage B in the same work-item, while the
 // request's value bytes are still in cache (a separate stage-B launch re-reads them
 // from HBM). Requests stage A can not prove gjson-equivalent go to the slow list.
-template <bool SHARED, bool EV>
+template <bool SHARED>
 __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
                                                       const uint32_t* __restrict__ set_of_req,
                                                       const uint8_t* __restrict__ arena,
@@ -363,7 +357,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
     if (k >= n) return;
     const RowRef row = wave_row(rows, row_stride, k);
     const uint8_t* d = arena + offs[r];
-    if (!scan_request<0, EV>(blob, d, lens[r], row, lane_ring(ring_off))) {
+    if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off))) {
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
@@ -386,7 +380,6 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
 // runs reads every table from LDS (each lane from its own run's copy), any other wave
 // reads them from global memory. Dynamic LDS: [staging region (ring_off bytes)] [rings].
 constexpr uint32_t kTenantRuns = 8;  // runs a workgroup may stage
-template <bool EV>
 __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_tenant(
     const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
@@ -440,7 +433,7 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     if (__all(ridx < nst)) {
         const uint8_t* blob = reinterpret_cast<const uint8_t*>(s_stage) + my_off;
         if (k >= n) return;
-        if (!scan_request<0, EV>(blob, d, lens[r], row, lane_ring(ring_off)) ||
+        if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off)) ||
             !finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
             row[0] = kRowSlow;
             slow_ids[atomicAdd(slow_count, 1u)] = r;
@@ -448,250 +441,12 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     } else {
         const uint8_t* gblob = sets[sid];
         if (k >= n) return;
-        if (!scan_request<0, EV>(gblob, d, lens[r], row, lane_ring(ring_off)) ||
+        if (!scan_request<0>(gblob, d, lens[r], row, lane_ring(ring_off)) ||
             !finish_request(r, gblob, d, row, out_tri, out_err, out_bm, stride)) {
             row[0] = kRowSlow;
             slow_ids[atomicAdd(slow_count, 1u)] = r;
         }
     }
-}
-
-// wavefront helpers of the lane kernel's window staging
-struct WaveHw {
-    __device__ uint32_t bpermute(uint32_t v, uint32_t src) const {
-        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
-    }
-    // the wavefront's LDS writes are visible to all its lanes
-    __device__ void lds_fence() const {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-};
-
-// ---------------------------------------------------------------------------------
-// The lane kernel (ajx_lane.h): one work-item per request, 64-byte windows staged by the
-// wavefront. Window w of the wave's 64 requests is four 1 KiB loads: in load q, lane l
-// brings the 16-byte block (l & 3) of window w of request 16 q + (l >> 2) — four lanes
-// read one request's 64 contiguous bytes, so one load instruction touches 16 documents —
-// and writes it to LDS at slot + q KiB + 16 l, which is where request 16 q + j finds its
-// window (q KiB + 64 j). Three slots per wave: window w - 1 (key bytes that started
-// there), window w (being scanned), window w + 1 (the byte after w; staged one window
-// ahead, at the start of iteration w, into the slot of w - 2). Latency: a wave waits for
-// its own window loads while the other waves of its SIMD scan (no registers held across
-// the scan). Dynamic LDS: [ruleset blob (SHARED)] [per wave 3 x 4 KiB].
-// MODE (profiling ablations, outputs meaningless): 1 the staging alone, 2 no token walk
-// and no stage B, 3 no key lookups, 4 no stage B.
-// ---------------------------------------------------------------------------------
-constexpr uint32_t kLaneBlock = 256;
-#ifndef AJX_LANE_WAVES
-#define AJX_LANE_WAVES 4  // waves per SIMD the lane kernel's register budget is set for
-#endif
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr uint32_t kLaneStageBytes = 3 * kLaneSlot;
-
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint32_t y = (uint32_t)__shfl_xor((int)v, o);
-        v = y > v ? y : v;
-    }
-    return v;
-}
-
-template <int MODE, bool SHARED>
-__global__ __launch_bounds__(kLaneBlock, AJX_LANE_WAVES) void ajx_lane_eval(
-    const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req, const uint8_t* __restrict__ arena,
-    const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n, uint64_t* __restrict__ rows,
-    uint32_t row_stride, uint32_t* __restrict__ slow_count, uint32_t* __restrict__ slow_ids,
-    uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm, uint32_t stride,
-    uint32_t blob_region, const uint32_t* __restrict__ perm) {
-    extern __shared__ uint4 s_lane[];
-    const uint8_t* blob0 = stage_blob<SHARED>(sets[0]);
-    WaveHw hw;
-    const uint32_t lane = threadIdx.x & 63u;
-    uint8_t* stage = reinterpret_cast<uint8_t*>(s_lane) + blob_region + (threadIdx.x >> 6) * kLaneStageBytes;
-    const uint32_t k = blockIdx.x * kLaneBlock + threadIdx.x;
-    const bool live = k < n;
-    const uint32_t r = live ? (perm ? perm[k] : k) : 0u;
-    const uint8_t* blob = SHARED ? blob0 : sets[set_of_req && live ? set_of_req[r] : 0];
-    const uint8_t* d = arena + (live ? offs[r] : 0);
-    const uint32_t len = live ? lens[r] : 0u;
-    const uint32_t mis = (uint32_t)((uintptr_t)d & 15u);
-    bool act = live && (reinterpret_cast<const RulesetHdr*>(blob)->flags & kFlagFastOk) && len < (1u << 24) && len;
-    const uint32_t nblk = act ? (mis + len + 15u) / 16u : 0u;
-    const uint32_t nwin = act ? (mis + len + kLaneWin - 1u) / kLaneWin : 0u;
-    const uint32_t nwmax = wave_max(nwin);
-    // the requests this lane loads for: 16 q + (lane >> 2), q = 0..3
-    const uintptr_t base = (uintptr_t)(d - mis);
-    const uint4* pb[4];
-    uint32_t pn[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const uint32_t src = 16u * (uint32_t)q + (lane >> 2);
-        const uint32_t lo = hw.bpermute((uint32_t)base, src), hi = hw.bpermute((uint32_t)((uint64_t)base >> 32), src);
-        pb[q] = reinterpret_cast<const uint4*>((uintptr_t)(((uint64_t)hi << 32) | lo));
-        pn[q] = hw.bpermute(nblk, src);
-    }
-    const uint32_t sub = lane & 3u;
-    auto load_win = [&](uint32_t w, uint4 (&v)[4]) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t b = w * 4u + sub;
-            if (b < pn[q]) {
-                const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pb[q]) + b);
-                v[q] = make_uint4(t.x, t.y, t.z, t.w);
-            } else {
-                v[q] = make_uint4(0u, 0u, 0u, 0u);
-            }
-        }
-    };
-    auto store_win = [&](uint32_t w, const uint4 (&v)[4]) {
-        uint4* s = reinterpret_cast<uint4*>(stage + (w % 3u) * kLaneSlot);
-#pragma unroll
-        for (int q = 0; q < 4; q++) s[q * 64 + lane] = v[q];
-    };
-    const uint32_t lane_off = (lane >> 4) * 1024u + (lane & 15u) * kLaneWin;
-    uint64_t* row = rows + (size_t)r * row_stride;
-    LaneScan sc;
-    if (act) sc.init(blob, blob_tables(blob), d, len, row);
-    sc.stage = (const AJX_LDS uint8_t*)stage;
-    sc.lane_off = lane_off;
-    uint32_t acc = 0;  // (MODE 1)
-    for (uint32_t w = 0; w < nwmax; w++) {
-        // stage window w (first iteration) and w + 1: the loads are waited for here;
-        // the other waves of the SIMD scan meanwhile
-        {
-            uint4 pf[4];
-            if (w == 0) {
-                load_win(0, pf);
-                store_win(0, pf);
-            }
-            if (w + 1 < nwmax) {
-                load_win(w + 1, pf);
-                store_win(w + 1, pf);
-            }
-            hw.lds_fence();
-        }
-        if (act && w < nwin) {
-            const uint4* s = reinterpret_cast<const uint4*>(stage + (w % 3u) * kLaneSlot + lane_off);
-            uint32_t x[16];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint4 v = s[j];
-                x[4 * j] = v.x;
-                x[4 * j + 1] = v.y;
-                x[4 * j + 2] = v.z;
-                x[4 * j + 3] = v.w;
-            }
-            if constexpr (MODE == 1) {
-#pragma unroll
-                for (int j = 0; j < 16; j++) acc ^= x[j];
-            } else {
-                sc.template window<MODE == 2 ? 2 : MODE == 3 ? 3 : 0>(x, w);
-                act = !sc.bad;
-            }
-        }
-        hw.lds_fence();  // every lane is done with window w - 1's slot before w + 2 lands there
-    }
-    if (!live) return;
-    if constexpr (MODE == 1) {
-        out_tri[r] = (uint8_t)acc;
-        return;
-    }
-    if (!act || !sc.finish()) {
-        row[0] = kRowSlow;
-        slow_ids[atomicAdd(slow_count, 1u)] = r;
-        return;
-    }
-    if constexpr (MODE == 2 || MODE == 4) {  // profiling: no stage B
-        out_tri[r] = (uint8_t)row[0];
-        return;
-    }
-    if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
-        row[0] = kRowSlow;
-        slow_ids[atomicAdd(slow_count, 1u)] = r;
-    }
-}
-
-hipError_t launch_eval_lane(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
-                            const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
-                            uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
-                            uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode, const uint32_t* d_perm, bool mods) {
-    if (n == 0) return hipSuccess;
-    const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
-    const uint32_t blob_region = shared ? (shared_blob_bytes + 15u) & ~15u : 0u;
-    const uint32_t lds = blob_region + (kLaneBlock / 64) * kLaneStageBytes;
-    if (lds > 160 * 1024 || (mode != 0 && !shared)) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
-    static std::atomic<uint64_t> attr_done{0};
-    e = attr_once(attr_done, [] {
-        const void* ks[] = {reinterpret_cast<const void*>(&ajx_lane_eval<0, true>),
-                            reinterpret_cast<const void*>(&ajx_lane_eval<0, false>),
-                            reinterpret_cast<const void*>(&ajx_lane_eval<1, true>),
-                            reinterpret_cast<const void*>(&ajx_lane_eval<2, true>),
-                            reinterpret_cast<const void*>(&ajx_lane_eval<3, true>),
-                            reinterpret_cast<const void*>(&ajx_lane_eval<4, true>)};
-        for (const void* k : ks) {
-            const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (r != hipSuccess) return r;
-        }
-        return hipSuccess;
-    });
-    if (e != hipSuccess) return e;
-    const uint32_t grid = (n + kLaneBlock - 1) / kLaneBlock;
-#define AJX_LANE_LAUNCH(M, S)                                                                                 \
-    hipLaunchKernelGGL((ajx_lane_eval<M, S>), dim3(grid), dim3(kLaneBlock), lds, stream, d_sets, d_set_of_req,    \
-                       d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, \
-                       stride, blob_region, d_perm)
-    if (mode == 1) AJX_LANE_LAUNCH(1, true);
-    else if (mode == 2) AJX_LANE_LAUNCH(2, true);
-    else if (mode == 3) AJX_LANE_LAUNCH(3, true);
-    else if (mode == 4) AJX_LANE_LAUNCH(4, true);
-    else if (shared)
-        hipLaunchKernelGGL((ajx_lane_eval<0, true>), dim3(grid), dim3(kLaneBlock), lds, stream, d_sets, d_set_of_req,
-                           d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                           stride, blob_region, d_perm);
-    else
-        hipLaunchKernelGGL((ajx_lane_eval<0, false>), dim3(grid), dim3(kLaneBlock), lds, stream, d_sets, d_set_of_req,
-                           d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                           stride, blob_region, d_perm);
-#undef AJX_LANE_LAUNCH
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (mode == 1 || mode == 2 || mode == 4) return hipSuccess;
-    const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
-    launch_slow_list(mods, sgrid, stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids,
-                     d_tri, d_err, d_bm, stride);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------
-// The row kernel (ajx_row.h): four documents per wavefront, 16 lanes each. Workgroups
-// of 4 waves stage the ruleset blob in LDS next to each wave's row buffers, then every
-// wave walks groups of four requests (grid-stride; the requests of a group are
-// consecutive in the length-bucketed order, so their lengths are alike). A tier takes
-// the documents that fit its row buffers (maxb); longer ones go to the next tier's list
-// (the last tier's "next" is the exact scan's list), as do the ones the row scan can not
-// prove. Output: each request's capture row (row r, header kRowSlow when handed over).
-// ---------------------------------------------------------------------------------
-hipError_t launch_eval_row(const uint8_t* const* d_sets, uint32_t blob_bytes, uint32_t n_selectors,
-                           const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
-                           uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
-                           uint32_t row_stride, uint32_t* d_slow, uint32_t* d_tier, hipStream_t stream,
-                           const uint32_t* d_perm, bool mods, int mode) {
-    if (n == 0) return hipSuccess;
-    if ((d_rows && row_stride < 1 + n_selectors) || n_selectors > 64u) return hipErrorInvalidValue;
-    hipError_t e = launch_row_scan(d_sets, blob_bytes, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_tri, d_err,
-                                   d_bm, stride, d_slow, d_tier, stream, d_perm);
-    if (e != hipSuccess) return e;
-    if (mode == 41) return hipSuccess;  // profiling: the row kernel alone
-    const uint32_t grid = (n + 255u) / 256u;
-    const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
-    launch_slow_list(mods, sgrid, stream, d_sets, nullptr, d_arena, d_offs, d_lens, d_slow, d_slow + 1, d_tri, d_err,
-                     d_bm, stride);
-    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
@@ -932,9 +687,6 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             int mode, const uint32_t* d_perm, bool mods) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
-    // stage A: the token scanner (ajx_fast.h); mode 31 the event scanner (ajx_events.h)
-    const bool ev = mode == 31;
-    if (mode == 31) mode = 0;
     // workgroup size by the waves a CU holds (each workgroup stages its own blob copy)
     uint32_t block = shared ? fast_block(shared_blob_bytes) : kFastBlock;
     if (mode >= 10 && mode <= 12) {  // profiling: the default kernel at a forced workgroup size
@@ -955,18 +707,15 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             reinterpret_cast<const void*>(&ajx_scan_fast<0, false>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<1, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<2, true>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused<true, true>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused<false, true>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused<true, false>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused<false, false>)};
+                            reinterpret_cast<const void*>(&ajx_scan_fused<true>),
+                            reinterpret_cast<const void*>(&ajx_scan_fused<false>)};
         for (const void* k : ks) {
             const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (r != hipSuccess) return r;
         }
         // (the tenant kernel also holds static LDS for __syncthreads_and: ask only for what
         // its launch uses, blob + four window rings)
-        for (const void* k : {reinterpret_cast<const void*>(&ajx_scan_fused_tenant<true>),
-                              reinterpret_cast<const void*>(&ajx_scan_fused_tenant<false>)}) {
+        for (const void* k : {reinterpret_cast<const void*>(&ajx_scan_fused_tenant)}) {
             const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      kMaxTenantStageBytes + 4 * kWinRingBytesPerWave);
             if (r != hipSuccess) return r;
@@ -998,15 +747,10 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
             hipLaunchKernelGGL((ajx_patterns<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
         }
-    } else if (shared) {  // the single-pass kernel (mode 0: token scanner; 31: event scanner)
-        if (ev)
-            hipLaunchKernelGGL((ajx_scan_fused<true, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
-                               d_bm, stride, ring_off, d_perm);
-        else
-            hipLaunchKernelGGL((ajx_scan_fused<true, false>), dim3(grid), dim3(block), lds, stream, d_sets,
-                               d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids,
-                               d_tri, d_err, d_bm, stride, ring_off, d_perm);
+    } else if (shared) {  // the single-pass kernel (token scanner)
+        hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride,
+                           ring_off, d_perm);
     } else if (d_set_of_req && shared_blob_bytes) {
         // multi-tenant batch (shared_blob_bytes != 0: staging on): each workgroup stages its
         // runs' rulesets, those that fit (ajx_scan_fused_tenant);
@@ -1015,22 +759,11 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
         // four groups still fit a CU)
         const uint32_t tblock = 256, tgrid = (n + tblock - 1) / tblock;
         const uint32_t toff = kMaxTenantStageBytes - 256u;
-        if (ev)
-            hipLaunchKernelGGL(ajx_scan_fused_tenant<true>, dim3(tgrid), dim3(tblock),
-                               toff + (tblock / 64) * kWinRingBytesPerWave, stream, d_sets, d_set_of_req, d_arena,
-                               d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                               stride, toff, d_perm);
-        else
-            hipLaunchKernelGGL(ajx_scan_fused_tenant<false>, dim3(tgrid), dim3(tblock),
-                               toff + (tblock / 64) * kWinRingBytesPerWave, stream, d_sets, d_set_of_req, d_arena,
-                               d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                               stride, toff, d_perm);
-    } else if (ev) {
-        hipLaunchKernelGGL((ajx_scan_fused<false, true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
-                           d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
-                           stride, ring_off, d_perm);
+        hipLaunchKernelGGL(ajx_scan_fused_tenant, dim3(tgrid), dim3(tblock), toff + (tblock / 64) * kWinRingBytesPerWave,
+                           stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count,
+                           d_slow_ids, d_tri, d_err, d_bm, stride, toff, d_perm);
     } else {
-        hipLaunchKernelGGL((ajx_scan_fused<false, false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+        hipLaunchKernelGGL((ajx_scan_fused<false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
                            d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
                            stride, ring_off, d_perm);
     }
@@ -1038,6 +771,28 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
     launch_slow_list(mods, sgrid, stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids,
                      d_tri, d_err, d_bm, stride);
+    return hipGetLastError();
+}
+
+// The row kernel's tiers (ajx_rowk.hip), then the exact scan of the requests they handed
+// over. Profiling modes: 41 the tiers alone; 42 / 43 / 44 stop the tiers after the
+// classification / the structure pass / row_finish (outputs meaningless).
+hipError_t launch_eval_row(const uint8_t* const* d_sets, uint32_t blob_bytes, uint32_t n_selectors,
+                           const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                           uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
+                           uint32_t row_stride, uint32_t* d_slow, uint32_t* d_tier, hipStream_t stream,
+                           const uint32_t* d_perm, bool mods, int mode) {
+    if (n == 0) return hipSuccess;
+    if ((d_rows && row_stride < 1 + n_selectors) || n_selectors > 64u) return hipErrorInvalidValue;
+    const uint32_t stop = mode >= 42 && mode <= 44 ? (uint32_t)(mode - 41) : 0u;
+    hipError_t e = launch_row_scan(d_sets, blob_bytes, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_tri, d_err,
+                                   d_bm, stride, d_slow, d_tier, stream, d_perm, stop);
+    if (e != hipSuccess) return e;
+    if (mode >= 41 && mode <= 44) return hipSuccess;
+    const uint32_t grid = (n + 255u) / 256u;
+    const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
+    launch_slow_list(mods, sgrid, stream, d_sets, nullptr, d_arena, d_offs, d_lens, d_slow, d_slow + 1, d_tri, d_err,
+                     d_bm, stride);
     return hipGetLastError();
 }
 

@@ -72,12 +72,13 @@ struct RowLayout {
     uint32_t maxb;  // document bytes a row can hold (multiple of 256, at most 8192)
     uint32_t maxe;  // events a row can hold
     uint32_t doc, doc_stride;
+    uint32_t doc2;  // a second set of document rows (the DMA of the next group), or = doc
     uint32_t ev, ev_stride;
     uint32_t bsb, bsb_stride;
     uint32_t stk, cap, misc;  // per-row strides: 32 x 4, 64 x 4, 16 x 4
     uint32_t bytes;           // the wave's whole region
 };
-AJW_HD RowLayout row_layout(uint32_t maxb, uint32_t maxe) {
+AJW_HD RowLayout row_layout(uint32_t maxb, uint32_t maxe, bool dbuf = false) {
     RowLayout L;
     L.maxb = maxb;
     L.maxe = maxe;
@@ -85,6 +86,11 @@ AJW_HD RowLayout row_layout(uint32_t maxb, uint32_t maxe) {
     L.doc = o;
     L.doc_stride = maxb + 32;
     o += kRowsPerWave * L.doc_stride;
+    L.doc2 = L.doc;
+    if (dbuf) {
+        L.doc2 = o;
+        o += kRowsPerWave * L.doc_stride;
+    }
     L.ev = o;
     L.ev_stride = ((maxe + 17) * 2 + 15) & ~15u;
     o += kRowsPerWave * L.ev_stride;
@@ -181,11 +187,14 @@ struct RowResult {
 // document. wl = the wave's LDS region. On return the capture data of each row is in
 // the row's cap words (start << 16 | end per selector, ~0 none) and `ok` says which rows
 // hold a valid capture.
-template <class Load>
-AJW M row_scan(const RowTabs& T, Lds wl, const RowLayout& L, M live, V len, V mis, Load load) {
+// PRE: the rows' documents are in the document rows at `docoff` already (the kernel's
+// LDS-DMA of the group); otherwise `load` reads them and P1 stores them there.
+template <bool PRE = false, class Load>
+AJW M row_scan(const RowTabs& T, Lds wl, const RowLayout& L, M live, V len, V mis, Load load, uint32_t stop = 0,
+               uint32_t docoff = 0xFFFFFFFFu) {
+    if (docoff == 0xFFFFFFFFu) docoff = L.doc;
     const V ln = lane(), row = ln >> 4, rl = ln & 15u;
-    const V rowlane15 = (row << 4) | 15u;
-    const V dbase = L.doc + row * L.doc_stride + 16u;  // docbuf offset of aligned byte 0
+    const V dbase = docoff + row * L.doc_stride + 16u;  // docbuf offset of aligned byte 0
     const V ebase = L.ev + row * L.ev_stride;
     const V bbase = L.bsb + row * L.bsb_stride;
     const V sbase = L.stk + row * (32u * 4u);
@@ -208,23 +217,27 @@ AJW M row_scan(const RowTabs& T, Lds wl, const RowLayout& L, M live, V len, V mi
     {
         V t = sel(ok, nsp, V(0u));
         t = row_max(t);
-        t = shfl(t, rowlane15);
+        t = row_bcast15(t);
         nsp_max = readlane(t, 15);
         nsp_max = nsp_max > readlane(t, 31) ? nsp_max : readlane(t, 31);
         nsp_max = nsp_max > readlane(t, 47) ? nsp_max : readlane(t, 47);
         nsp_max = nsp_max > readlane(t, 63) ? nsp_max : readlane(t, 63);
     }
     V c_esc = V(0u), c_str = V(0u), c_s15 = V(0u), c_qc15 = V(0u), c_cnt = V(0u);
-    G16 nx = load(rl, ok & (rl < nblk));
+    G16 nx;
+    if (!PRE) nx = load(rl, ok & (rl < nblk));
     for (uint32_t sp = 0; sp < nsp_max; sp++) {
-        const G16 x = nx;
         const V b = sp * 16u + rl;
         const M vb = ok & (b < nblk);
-        {
+        G16 x;
+        if (PRE) {
+            x = ld128(wl, dbase + sel(vb, b, V(0u)) * 16u);
+        } else {
+            x = nx;
             const V bn = b + 16u;
             nx = load(bn, ok & (bn < nblk));
+            st128(wl, vb, dbase + b * 16u, x.x, x.y, x.z, x.w);
         }
-        st128(wl, vb, dbase + b * 16u, x.x, x.y, x.z, x.w);
         // valid bytes of the block: doc positions b*16 - mis + k in [0, len)
         const V lo = sel(b == 0u, mis, V(0u));
         const V hi_raw = len + mis - b * 16u;  // (vb: > 0)
@@ -266,7 +279,7 @@ AJW M row_scan(const RowTabs& T, Lds wl, const RowLayout& L, M live, V len, V mi
             const V cin = sel(rl == 0u, c_esc, row_shr<1>(co0));
             V co;
             escaped = esc_of(BS, cin, co);
-            c_esc = shfl(co, rowlane15) & sel(ok, V(1u), V(0u));
+            c_esc = row_bcast15(co) & sel(ok, V(1u), V(0u));
         }
         st16(wl, vb & (rl == 0u), bbase + sp * 2u, row_bits(bsb_ballot, row));
         // strings
@@ -289,15 +302,15 @@ AJW M row_scan(const RowTabs& T, Lds wl, const RowLayout& L, M live, V len, V mi
         bad = bad | (QO & ~prevS);
         const V prevQC = ((QC << 1) | sel(rl == 0u, c_qc15, row_shr<1>(QC >> 15))) & 0xFFFFu;
         bad = bad | (prevQC & ~So & vm);
-        c_s15 = shfl(So >> 15, rowlane15);
-        c_qc15 = shfl(QC >> 15, rowlane15);
+        c_s15 = row_bcast15(So >> 15);
+        c_qc15 = row_bcast15(QC >> 15);
         min32(wl, vb & (bad != 0u), mbase + MS_BADPOS * 4u, p0 + ctz(bad));
         // events
         V E = So;
         const V cnt = popc(E);
         const V incl = row_sum(cnt);
         V idx = c_cnt + incl - cnt;
-        c_cnt = c_cnt + shfl(incl, rowlane15);
+        c_cnt = c_cnt + row_bcast15(incl);
         while (any(E != 0u)) {
             const M m = E != 0u;
             const V k = ctz(E);
@@ -322,12 +335,13 @@ AJW M row_scan(const RowTabs& T, Lds wl, const RowLayout& L, M live, V len, V mi
     }
 
     AJW_TRACE(live & !ok, "not ok after P1");
+    if (stop == 1) return ok;  // (profiling: P1 alone)
     // ---- P2: events
     const V nr = (cnt + 15u) >> 4;
     uint32_t nr_max = 0;
     {
         V t = row_max(sel(ok, nr, V(0u)));
-        t = shfl(t, rowlane15);
+        t = row_bcast15(t);
         for (uint32_t r = 0; r < 4; r++) nr_max = nr_max > readlane(t, 16 * r) ? nr_max : readlane(t, 16 * r);
     }
     V dc = V(0u), pcode = V(0u), ppos = V(0u), pnode = V(kNodeNone);
@@ -448,8 +462,8 @@ AJW M row_scan(const RowTabs& T, Lds wl, const RowLayout& L, M live, V len, V mi
         // containers, level by level (a container's node before the keys inside it)
         V Lmin_v = row_max(sel(act, 64u - pre, V(0u)));
         V Lmax_v = row_max(sel(act, vmax(pre, post), V(0u)));
-        Lmin_v = shfl(Lmin_v, rowlane15);
-        Lmax_v = shfl(Lmax_v, rowlane15);
+        Lmin_v = row_bcast15(Lmin_v);
+        Lmax_v = row_bcast15(Lmax_v);
         uint32_t Lmin = 64, Lmax = 0;
         for (uint32_t r = 0; r < 4; r++) {
             const uint32_t a = 64u - readlane(Lmin_v, 16 * r), bmax = readlane(Lmax_v, 16 * r);
@@ -541,24 +555,25 @@ AJW M row_scan(const RowTabs& T, Lds wl, const RowLayout& L, M live, V len, V mi
         AJW_TRACEV(act & !valid, "  pre", pre);
         // carries
         rootpos = sel(is_root_close, pos, rootpos);
-        rootpos = shfl(row_max(rootpos), rowlane15);
+        rootpos = row_bcast15(row_max(rootpos));
         done = done | (rc != 0u);
-        dc = shfl(post, rowlane15);
-        pcode = shfl(code, rowlane15);
-        ppos = shfl(pos, rowlane15);
-        pnode = shfl(node, rowlane15);
+        dc = row_bcast15(post);
+        pcode = row_bcast15(code);
+        ppos = row_bcast15(pos);
+        pnode = row_bcast15(node);
         lds_fence();
     }
     {
         const V rj = row_max(sel(rej, V(1u), V(0u)));
         AJW_TRACE(ok & !done, "root not closed");
-        ok = ok & done & (shfl(rj, rowlane15) == 0u);
+        ok = ok & done & (row_bcast15(rj) == 0u);
     }
     // problems P1 saw before the root's close
     AJW_TRACE(ok & (ld32(wl, mbase + MS_BADPOS * 4u) <= rootpos), "P1 local rule");
     ok = ok & (ld32(wl, mbase + MS_BADPOS * 4u) > rootpos);
 
     AJW_TRACE(live & !ok, "not ok after P2");
+    if (stop == 2) return ok;  // (profiling: P1 + P2)
     // ---- post pass: atoms of indexed arrays. Element k of an array whose events right
     // after its open are k commas is the gap after the k-th one (the open for k = 0).
     if (T.n_idx != 0) {
@@ -596,7 +611,7 @@ AJW M row_scan(const RowTabs& T, Lds wl, const RowLayout& L, M live, V len, V mi
             }
         }
         const V rj = row_max(sel(rej, V(1u), V(0u)));
-        ok = ok & (shfl(rj, rowlane15) == 0u);
+        ok = ok & (row_bcast15(rj) == 0u);
     }
     return ok;
 }
@@ -627,10 +642,11 @@ AJW RowTabs row_tabs(const uint8_t* gblob, Lds lblob) {
 // whitespace (gjson would stop there) are dropped from `ok`. hdr_lo/hdr_hi: the found
 // bits of the row.
 template <class Emit>
-AJW M row_finish(const RowTabs& T, Lds wl, const RowLayout& L, M ok, V mis, V& hdr_lo, V& hdr_hi, Emit emit) {
+AJW M row_finish(const RowTabs& T, Lds wl, const RowLayout& L, M ok, V mis, V& hdr_lo, V& hdr_hi, Emit emit,
+                 uint32_t docoff = 0xFFFFFFFFu) {
+    if (docoff == 0xFFFFFFFFu) docoff = L.doc;
     const V ln = lane(), row = ln >> 4, rl = ln & 15u;
-    const V rowlane15 = (row << 4) | 15u;
-    const V dbase = L.doc + row * L.doc_stride + 16u;
+    const V dbase = docoff + row * L.doc_stride + 16u;
     const V dmis = dbase + mis;
     const V bbase = L.bsb + row * L.bsb_stride;
     const V cbase = L.cap + row * (kRowMaxSel * 4u);
@@ -701,7 +717,7 @@ AJW M row_finish(const RowTabs& T, Lds wl, const RowLayout& L, M ok, V mis, V& h
         emit(s, m, found, start, end - start, type, sel(esc, V(1u), V(0u)));
     }
     const V rj = row_max(sel(rej, V(1u), V(0u)));
-    return ok & (shfl(rj, rowlane15) == 0u);
+    return ok & (row_bcast15(rj) == 0u);
 }
 
 // Stage B in the row kernel: Pattern.Matches (pkg/jsonexp/expressions.go:59-96) of every
@@ -714,10 +730,10 @@ AJW M row_finish(const RowTabs& T, Lds wl, const RowLayout& L, M ok, V mis, V& h
 // bitmap words.
 template <class OutFn, class BmFn>
 AJW M row_patterns(const uint8_t* blob, Lds wl, const RowLayout& L, M ok, V mis, V r, OutFn out, BmFn bm,
-                   uint32_t bm_words) {
+                   uint32_t bm_words, uint32_t docoff = 0xFFFFFFFFu) {
+    if (docoff == 0xFFFFFFFFu) docoff = L.doc;
     const V ln = lane(), row = ln >> 4, rl = ln & 15u;
-    const V rowlane15 = (row << 4) | 15u;
-    const V dmis = L.doc + row * L.doc_stride + 16u + mis;
+    const V dmis = docoff + row * L.doc_stride + 16u + mis;
     const V cbase = L.cap + row * (kRowMaxSel * 4u);
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const Pattern* pats = reinterpret_cast<const Pattern*>(blob + h->off_patterns);
@@ -753,6 +769,8 @@ AJW M row_patterns(const uint8_t* blob, Lds wl, const RowLayout& L, M ok, V mis,
                         const bool mm = raw.lit ? dfa_match_lit(blob, pt.dfa_off, raw.lit)
                                                 : dfa_match_span(blob, pt.dfa_off, doc + raw.a, raw.n);
                         rv = mm ? V_T : V_F;
+                    } else if ((pt.op == OP_INCL || pt.op == OP_EXCL) && v.type == T_NULL) {
+                        rv = pt.op == OP_EXCL ? V_T : V_F;  // Array() of Null is empty
                     } else if ((pt.op == OP_INCL || pt.op == OP_EXCL) && raw.ok &&
                                !(v.type == T_JSON && doc[v.start] == '[')) {
                         // Array() of a value that is not an array: the value alone
@@ -819,7 +837,6 @@ AJW M row_patterns(const uint8_t* blob, Lds wl, const RowLayout& L, M ok, V mis,
             bm(AJW_L(r), kk, word);
         }
     }
-    (void)rowlane15;
     return ok;
 }
 

@@ -99,6 +99,25 @@ AJW void lds_fence() {
 struct G16 {
     V x, y, z, w;
 };
+AJW G16 ld128(Lds b, V o) {
+    const ajw_u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const ajw_u32x4*>(b + o);
+    return G16{v.x, v.y, v.z, v.w};
+}
+// LDS-DMA: 16 bytes from each active lane's global address p to dst + 16 * lane (dst is
+// wave-uniform; global_load_lds_dwordx4, counted in vmcnt)
+AJW void dma16(const uint8_t* p, Lds dst, M m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (m) __builtin_amdgcn_global_load_lds((const void*)p, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+#else
+    (void)p; (void)dst; (void)m;
+#endif
+}
+// wait for every vector memory operation of the wave (the DMA above included)
+AJW void wait_vm() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+#endif
+}
 AJW G16 gld128(const uint8_t* p, M m) {
     if (m) {
         const uint4 v = *reinterpret_cast<const uint4*>(p);
@@ -295,6 +314,18 @@ AJW const uint8_t* gptr(Lds b, uint32_t o) { return b + o; }
 struct G16 {
     V x, y, z, w;
 };
+AJW G16 ld128(Lds b, const V& o) {
+    G16 r;
+    for (int l = 0; l < 64; l++) {
+        uint32_t t[4];
+        std::memcpy(t, b + o.x[l], 16);
+        r.x.x[l] = t[0];
+        r.y.x[l] = t[1];
+        r.z.x[l] = t[2];
+        r.w.x[l] = t[3];
+    }
+    return r;
+}
 // per-lane global addresses: the host build passes them as 64 pointers
 struct P {
     const uint8_t* p[64];
@@ -384,6 +415,12 @@ AJW V row_max(V v) {
     v = vmax(v, row_shr<4>(v));
     v = vmax(v, row_shr<8>(v));
     return v;
+}
+// the value lane 15 of each lane's row holds (four readlanes: no LDS round trip)
+AJW V row_bcast15(V v) {
+    const uint32_t a = readlane(v, 15), b = readlane(v, 31), c = readlane(v, 47), d = readlane(v, 63);
+    const V row = lane() >> 4;
+    return sel(row == 0u, V(a), sel(row == 1u, V(b), sel(row == 2u, V(c), V(d))));
 }
 // the 16 bits of ballot `b` that belong to each lane's row
 AJW V row_bits(uint64_t b, V row) {

@@ -131,6 +131,10 @@ class AuthResult:
     metadata: Dict[str, object] = field(default_factory=dict)  # success: dynamic metadata
 
 
+def _paths_select_authorization(paths) -> bool:
+    return any(p == "auth.authorization" or p.startswith("auth.authorization.") for p in paths)
+
+
 def _selects_authorization(expr: Optional[jsonexp.Expression]) -> bool:
     if expr is None:
         return False
@@ -154,8 +158,17 @@ class AuthPipelineBatch:
                 self._rs[id(e)] = self.ctx.compile_expression(e)
         prios = sorted({c.priority for c in auth_config.authorization})
         self.levels = [[c for c in auth_config.authorization if c.priority == p] for p in prios]
-        self._needs_regen = any(_selects_authorization(e) for lvl in self.levels[1:] for c in lvl
-                                for e in (c.conditions, c.rules))
+        # a later priority reads what an earlier one granted (auth.authorization.*): its
+        # conditions and rules, its cache keys (ResolveKeyFor on GetAuthorizationJSON,
+        # authorization.go:56-66), and denyWith, which resolves on the JSON of the priority
+        # that denied (auth_pipeline.go:581-608): the documents must be rebuilt per level
+        dw = auth_config.unauthorized
+        self._needs_regen = (
+            any(_selects_authorization(e) for lvl in self.levels[1:] for c in lvl for e in (c.conditions, c.rules))
+            or any(c.cache is not None and _paths_select_authorization(c.cache.key.paths())
+                   for lvl in self.levels[1:] for c in lvl)
+            or (dw is not None and len(self.levels) > 1
+                and any(v is not None and _paths_select_authorization(v.paths()) for v in dw.values())))
         # one forest ruleset for every expression of the phase when no later priority reads
         # what an earlier one granted: one document scan per request for all of them
         self._forest = None

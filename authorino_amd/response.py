@@ -38,7 +38,7 @@ NULL, FALSE, NUMBER, STRING, TRUE, JSON = 0, 1, 2, 3, 4, 5
 UNSUPPORTED = 255
 
 _ALL_CURLY = re.compile(r"{")                      # json.go:18
-_MODIFIER_CURLY = re.compile(r"[^@]+@\w+:{")       # json.go:19
+_MODIFIER_CURLY = re.compile(r"[^@]+@\w+:{", re.ASCII)  # json.go:19 (Go's \w is ASCII)
 
 RESPONSE_PLAIN = "plain"      # pkg/evaluators/response.go (responsePlain)
 RESPONSE_JSON = "json"        # responseJSON

@@ -308,7 +308,9 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    if world > 1:
+    # RCCL for N > 1 ranks, and for one rank started by torch.distributed.run with
+    # --gather-decisions (the single-GPU rehearsal of the N-rank path)
+    if world > 1 or (args.gather_decisions and "WORLD_SIZE" in os.environ):
         import torch.distributed as dist
 
         torch.cuda.set_device(local)

@@ -219,7 +219,8 @@ int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* set
 /* The values of patterns [first_pattern, first_pattern + values_stride) of `rs` from the
  * capture rows the last authjx_eval_batch_device call on this context wrote: that call
  * must have evaluated `rs` alone over the same d_arena / d_offs / d_lens (n requests),
- * without authjx_set_exact_scan. For a phase compiled with authjx_compile_forest whose
+ * without authjx_set_exact_scan, and `rs` must come from authjx_compile_forest (the
+ * default kernel keeps capture rows for forests only). For a phase compiled with authjx_compile_forest whose
  * last tree holds the response selectors (AUTHJX_OP_EQ patterns, root -1), this resolves
  * them without a second document scan: the gjson.Get of JSONValue.ResolveFor
  * (pkg/json/json.go:41-53) after the rules of the same request. AUTHJX_EINVAL when the

@@ -142,10 +142,8 @@ def _fast_decl():
         L.ht_eval_fast.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8),
                                    C.POINTER(C.c_int32)]
         L.ht_eval_fast.restype = C.c_int
-        L.ht_eval_ev.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8),
-                                 C.POINTER(C.c_int32), C.c_void_p]
-        L.ht_eval_ev.restype = C.c_int
-        L.ht_eval_tok.argtypes = L.ht_eval_ev.argtypes
+        L.ht_eval_tok.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8),
+                                  C.POINTER(C.c_int32), C.c_void_p]
         L.ht_eval_tok.restype = C.c_int
         L._fast_declared = True
     return L
@@ -161,64 +159,16 @@ def eval_fast(hr: "HostRuleset", doc, mis: int = 0):
     return t, err.value, list(res)[: hr.n]
 
 
-def eval_ev(hr: "HostRuleset", doc, mis: int = 0, n_sel: int = 0, token_scanner: bool = False):
-    """Single-pass path with the event scanner (or the token scanner) on the host: (tri |
-    -1 slow | -2 not eligible, err, res, capture row [found, records...] or None)."""
+def eval_tok(hr: "HostRuleset", doc, mis: int = 0, n_sel: int = 0):
+    """The token-scanner single-pass path on the host: (tri | -1 slow | -2 not eligible,
+    err, res, capture row [found, records...] or None)."""
     L = _fast_decl()
     d = _b(doc)
     res = (C.c_uint8 * max(hr.n, 1))()
     err = C.c_int32(-1)
     row = (C.c_uint64 * (1 + max(n_sel, 64)))()
-    f = L.ht_eval_tok if token_scanner else L.ht_eval_ev
-    t = f(hr._h, d, len(d), mis, res, C.byref(err), C.cast(row, C.c_void_p))
+    t = L.ht_eval_tok(hr._h, d, len(d), mis, res, C.byref(err), C.cast(row, C.c_void_p))
     return t, err.value, list(res)[: hr.n], (list(row)[: 1 + n_sel] if t >= 0 else None)
-
-
-_W = None
-
-
-def lane_lib():
-    """tests/native/libajx_lanetest.so: the lane kernel's scanner on the host."""
-    global _W
-    if _W is None:
-        subprocess.run(["make", "-s", "-C", _NATIVE], check=True)
-        L = C.CDLL(os.path.join(_NATIVE, "libajx_lanetest.so"))
-        L.hw_compile.argtypes = [C.POINTER(_Tree), C.POINTER(C.c_int)]
-        L.hw_compile.restype = C.c_void_p
-        L.hw_free.argtypes = [C.c_void_p]
-        L.hw_lane_ok.argtypes = [C.c_void_p]
-        L.hw_lane_ok.restype = C.c_int
-        L.hw_eval_lane.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint8, C.POINTER(C.c_uint8),
-                                   C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
-        L.hw_eval_lane.restype = C.c_int
-        _W = L
-    return _W
-
-
-class LaneRuleset:
-    """A ruleset for the lane-kernel harness: eval(doc) -> (tri | -1 exact scan | -2 not
-    eligible, err, per-pattern results, capture row)."""
-
-    def __init__(self, patterns, nodes, root):
-        self.n = len(patterns)
-        t, self._keep = make_tree(patterns, nodes, root)
-        rc = C.c_int(0)
-        self._h = lane_lib().hw_compile(C.byref(t), C.byref(rc))
-        self.rc = rc.value
-        self.ok = bool(self._h) and bool(lane_lib().hw_lane_ok(self._h))
-
-    def eval(self, doc, mis=0, fill=0x41):
-        d = _b(doc)
-        res = (C.c_uint8 * max(self.n, 1))()
-        err = C.c_int32(-1)
-        row = (C.c_uint64 * 260)()
-        nwin = C.c_uint32(0)
-        t = lane_lib().hw_eval_lane(self._h, d, len(d), mis, fill, res, C.byref(err), row, C.byref(nwin))
-        return t, err.value, list(res)[: self.n], list(row)
-
-    def __del__(self):
-        if getattr(self, "_h", None):
-            lane_lib().hw_free(self._h)
 
 
 def _row_decl():

@@ -18,7 +18,7 @@
 #include <random>
 #include <string>
 
-#include "../../authorino_amd/csrc/ajx_device.h"
+#include "../../authorino_amd/csrc/ajx_fast.h"
 
 extern "C" {
 #include "../../oracle/oracle.h"
@@ -67,7 +67,28 @@ static std::string go_text(double f) {  // FormatFloat(f, 'g'-like) via the orac
     return out;
 }
 
+// --stdin: one number text per line in, "device<TAB>oracle<TAB>raw-fast" out (raw-fast:
+// 1 when the single-pass kernels' raw rule, -?[0-9]+ or a simple decimal, takes the text
+// as its own String()), for an independent check of both against numpy/Python
+static int stdin_mode() {
+    static char line[4096];
+    while (fgets(line, sizeof line, stdin)) {
+        size_t n = strlen(line);
+        while (n && (line[n - 1] == '\n' || line[n - 1] == '\r')) line[--n] = 0;
+        const std::string raw(line, n);
+        uint32_t k = 0;
+        if (k < n && raw[k] == '-') k++;
+        bool integer = k < n;
+        for (uint32_t j = k; j < n; j++)
+            if (raw[j] < '0' || raw[j] > '9') integer = false;
+        const bool fast = integer || simple_decimal((const uint8_t*)raw.data() + k, (uint32_t)(n - k));
+        printf("%s\t%s\t%d\n", device_string(raw).c_str(), oracle_string(raw).c_str(), fast ? 1 : 0);
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && strcmp(argv[1], "--stdin") == 0) return stdin_mode();
     const long N = argc > 1 ? atol(argv[1]) : 100000;
     const unsigned seed = argc > 2 ? (unsigned)atol(argv[2]) : 1;
     std::mt19937_64 rng(seed);

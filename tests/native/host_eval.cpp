@@ -8,7 +8,6 @@
 #include <vector>
 
 #include "../../authorino_amd/csrc/ajx_compiler.h"
-#include "../../authorino_amd/csrc/ajx_events.h"
 #include "../../authorino_amd/csrc/ajx_fast.h"
 #include "../../authorino_amd/csrc/ajx_modifiers.h"
 #include "../../authorino_amd/csrc/ajx_regex.h"
@@ -185,12 +184,6 @@ int ht_eval_tok(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t
                 uint64_t* row_out) {
     return eval_single_pass(h, doc, len, mis, res, err, false, row_out);
 }
-// the same with the event scanner (ajx_events.h) for stage A; row_out (1 + n_selectors):
-// the capture row when the request stays on the single-pass path
-int ht_eval_ev(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
-               uint64_t* row_out) {
-    return eval_single_pass(h, doc, len, mis, res, err, true, row_out);
-}
 static int eval_single_pass(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
                             bool ev, uint64_t* row_out) {
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
@@ -209,8 +202,8 @@ static int eval_single_pass(void* h, const uint8_t* doc, uint32_t len, uint32_t 
         if (b < nblk) return Block16{a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
         return Block16{0, 0, 0, 0};
     };
-    const bool ok = ev ? scan_doc_ev(blob, blob_tables(blob), d, len, row.data(), ring, load)
-                       : scan_doc(blob, blob_tables(blob), d, len, row.data(), ring, load);
+    (void)ev;
+    const bool ok = scan_doc(blob, blob_tables(blob), d, len, row.data(), ring, load);
     if (!ok) return -1;
     if (row_out) std::memcpy(row_out, row.data(), row.size() * sizeof(uint64_t));
     uint64_t t[2], u[2];

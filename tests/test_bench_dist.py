@@ -4,6 +4,7 @@ shards are independent (different documents per rank, no data-path collective)."
 import json
 import os
 import socket
+import subprocess
 import sys
 import time
 
@@ -128,3 +129,31 @@ def test_decision_bitmap_on_device():
     got = bench.decision_bitmap(torch, tri.cuda(), 1, wts.cuda()).cpu()
     assert torch.equal(got, want)
     assert int(want[0]) == sum(1 << k for k in range(8) if int(tri[k]) == 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_rccl_gather_one_rank_on_device():
+    """The real multi-GPU driver at world size 1: bench.py under torch.distributed.run
+    (a child process started before anything here touches the GPU), RCCL process group
+    with device_id, the decision bitmap all-gathered on the bench stream inside the timed
+    step; the JSON line, the gathered slice equal to the rank's own bitmap, and parity of
+    the shard against the oracle sample."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--gather-decisions", "--steps", "2", "--warmup", "1", "--requests", "65536",
+           "--cpu-seconds", "2", "--no-pcie"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = lines[0]
+    g = rec["decision_gather"]
+    assert g["ranks"] == 1 and g["slices_equal_to_local"]
+    assert g["bytes_per_rank"] * 8 == rec["config"]["requests_per_gpu"] * rec["config"]["trees_per_request"]
+    assert rec["parity"]["mismatches"] == 0 and rec["parity"]["sample"] > 0
+    assert rec["undecided"] == 0

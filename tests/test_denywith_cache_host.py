@@ -182,3 +182,38 @@ def test_batched_cache_equals_serial_requests():
     for b, s in zip(batched, serial):
         assert (b.code, b.message, b.authorization) == (s.code, s.message, s.authorization)
     assert any(b.code == P.CODE_OK for b in batched) and any(b.code != P.CODE_OK for b in batched)
+
+
+def test_later_reads_of_granted_objects_need_a_producer():
+    """A cache key at a later priority, or denyWith over more than one priority, that reads
+    auth.authorization.* resolves on the JSON with the earlier priorities' grants
+    (authorization.go:56-66, auth_pipeline.go:581-608): the batch rebuilds the documents
+    through the producer, and refuses to run without one (no key collides on a missing
+    grant)."""
+    import pytest
+
+    allow = J.All(J.Pattern("auth.identity.sub", J.EqualOperator, "alice"))
+    first = P.AuthorizationConfig("first", rules=allow, priority=0)
+    keyed = P.AuthorizationConfig("second", rules=allow, priority=1,
+                                  cache=CA.EvaluatorCache(JSONValue(pattern="auth.authorization.first"), ttl=60))
+    cfg = P.AuthConfig(authorization=[first, keyed])
+    with pytest.raises(ValueError):
+        P.AuthPipelineBatch(cfg, ctx=OracleCtx()).evaluate([_req()])
+    # the same key at the first priority reads nothing granted yet: no producer needed
+    keyed0 = P.AuthorizationConfig("second", rules=allow, priority=0,
+                                   cache=CA.EvaluatorCache(JSONValue(pattern="auth.authorization.first"), ttl=60))
+    (r,) = P.AuthPipelineBatch(P.AuthConfig(authorization=[first, keyed0]), ctx=OracleCtx()).evaluate([_req()])
+    assert r.code != P.CODE_PERMISSION_DENIED
+    dw = P.DenyWithValues(message=JSONValue(pattern="auth.authorization.first"))
+    cfg = P.AuthConfig(authorization=[first, P.AuthorizationConfig("deny", rules=_deny_all().rules, priority=1)],
+                       unauthorized=dw)
+    with pytest.raises(ValueError):
+        P.AuthPipelineBatch(cfg, ctx=OracleCtx()).evaluate([_req()])
+
+    def producer(i, granted):
+        d = json.loads(_req())
+        d["auth"]["authorization"] = granted
+        return json.dumps(d, separators=(",", ":")).encode()
+
+    (r,) = P.AuthPipelineBatch(cfg, ctx=OracleCtx()).evaluate([_req()], producer=producer)
+    assert r.code == P.CODE_PERMISSION_DENIED and r.message == "true"

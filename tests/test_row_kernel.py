@@ -83,7 +83,7 @@ def test_row_capture_rows_equal_token_scanner():
             rc, rows = H.scan_rows(hr, docs, mis, ns)
             assert rc == len(docs)
             for d, m, row in zip(docs, mis, rows):
-                t = H.eval_ev(hr, d, mis=m, n_sel=ns, token_scanner=True)
+                t = H.eval_tok(hr, d, mis=m, n_sel=ns)
                 assert t[0] >= 0
                 tok = t[3]
                 assert row[0] == tok[0], (workload, d)
@@ -192,3 +192,41 @@ def test_row_kernel_limits():
     assert _check(rs, hr, d)[0] == 1
     assert _check(rs, hr, d, maxe=32)[0] == -1       # more events than the row holds
     assert _check(rs, hr, d, maxb=256)[0] == -1      # longer than the row buffer
+
+
+@pytest.mark.parametrize("seed", [77, 78])
+def test_row_kernel_random_trees_match_oracle(seed):
+    """Random And/Or trees over random selectors, documents with whitespace and mutations
+    (the GPU suite's test_random_documents_and_selectors, per document): tri-state, error
+    pattern and per-pattern results equal the oracle wherever the row kernel decides —
+    Null values included (Array() of Null is empty: excl true, incl false)."""
+    rng = np.random.default_rng(seed)
+    kept = 0
+    for _ in range(50):
+        pats = FU.rand_patterns(rng, int(rng.integers(1, 10)))
+        nodes = [(0, -1, -1, i) for i in range(len(pats))]
+        root = -1
+        for i in reversed(range(len(pats))):
+            nodes.append((2 if rng.random() < 0.3 else 1, i, root, -1))
+            root = len(nodes) - 1
+        ors, hr = O.Ruleset(pats, nodes, root), H.HostRuleset(pats, nodes, root)
+        for _ in range(60):
+            d = FU.rand_doc(rng)
+            d = FU.mutate(rng, d) if rng.random() < 0.3 else d
+            ot = [ors.pattern(p, d) for p in range(len(pats))]
+            if O.UNSUPPORTED in ot:
+                continue
+            t, e, res = H.eval_row(hr, d, mis=int(rng.integers(0, 16)))
+            if t < 0:
+                continue
+            kept += 1
+            assert (t, e) == ors.matches(d), (pats, nodes, root, d)
+            assert res == ot, (pats, d)
+    assert kept > 600
+
+
+def test_row_kernel_incl_excl_on_null_and_scalars():
+    pats = [("n", 3, ""), ("n", 4, ""), ("s", 3, "x"), ("s", 4, "x"), ("o", 3, '{"a":1}'), ("m", 4, "")]
+    rs, hr = _rulesets(pats)
+    for d in [b'{"n":null,"s":"x","o":{"a":1}}', b'{"n":[null],"s":["y","x"],"o":[{"a":1}]}', b'{"s":1}']:
+        _check(rs, hr, d)
