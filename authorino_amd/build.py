@@ -16,8 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libauthjx.so")
 INCLUDE_H = os.path.join(HERE, "..", "include", "authjx.h")
-SOURCES = ["ajx_regex.cpp", "ajx_compiler.cpp", "ajx_api.cpp", "ajx_index.cpp", "ajx_producer.cpp", "ajx_kernels.hip",
-           "ajx_rowk.hip"]
+SOURCES = ["ajx_regex.cpp", "ajx_compiler.cpp", "ajx_api.cpp", "ajx_index.cpp", "ajx_producer.cpp", "ajx_kernels.hip"]
 ARCH = os.environ.get("AUTHJX_ARCH", "gfx950")
 _INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
 

@@ -48,8 +48,6 @@ struct Workspace {
     size_t rows_cap = 0;         // in u64
     uint32_t* d_perm = nullptr;  // length-bucketed request order (+ 2 x 1024 + 1 u32 histogram)
     uint32_t perm_cap = 0;
-    uint32_t* d_tier = nullptr;  // the row kernel's tier lists: 2 x ([0] count + n ids)
-    uint32_t tier_cap = 0;
     // the capture rows in d_rows: written by the last single-ruleset, full evaluation of
     // rows_rs over rows_n requests on this stream (nullptr: none usable)
     const authjx_ruleset* rows_rs = nullptr;
@@ -130,7 +128,6 @@ void destroy_workspace(Workspace* w) {
     if (w->d_slow) (void)hipFree(w->d_slow);
     if (w->d_rows) (void)hipFree(w->d_rows);
     if (w->d_perm) (void)hipFree(w->d_perm);
-    if (w->d_tier) (void)hipFree(w->d_tier);
     if (w->ev0) (void)hipEventDestroy(w->ev0);
     if (w->ev1) (void)hipEventDestroy(w->ev1);
     delete w;
@@ -167,7 +164,7 @@ int ensure_sets(Workspace* w, int device, const authjx_ruleset* const* sets, uin
 int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
     // (rows for whole waves: the fused kernels' wave-interleaved layout)
     const size_t rows_need = (size_t)((n + 63u) & ~63u) * row_stride;
-    if (n <= w->slow_cap && n <= w->perm_cap && n <= w->tier_cap && rows_need <= w->rows_cap) return AUTHJX_OK;
+    if (n <= w->slow_cap && n <= w->perm_cap && rows_need <= w->rows_cap) return AUTHJX_OK;
     HIP_OK(hipStreamSynchronize(w->stream));
     w->rows_rs = nullptr;
     if (n > w->slow_cap) {
@@ -183,13 +180,6 @@ int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
         w->perm_cap = 0;
         HIP_OK(hipMalloc(&w->d_perm, ((size_t)n + 4096) * sizeof(uint32_t)));
         w->perm_cap = n;
-    }
-    if (n > w->tier_cap) {
-        if (w->d_tier) (void)hipFree(w->d_tier);
-        w->d_tier = nullptr;
-        w->tier_cap = 0;
-        HIP_OK(hipMalloc(&w->d_tier, 2 * ((size_t)n + 1) * sizeof(uint32_t)));
-        w->tier_cap = n;
     }
     if (rows_need > w->rows_cap) {
         if (w->d_rows) (void)hipFree(w->d_rows);
@@ -380,22 +370,12 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         if (rc != AUTHJX_OK) return rc;
     }
     HIP_OK(hipEventRecord(w->ev0, s));
-    // kernel: the row kernel (default for a batch over one ruleset, ajx_row.h); the
-    // token-scanner single-pass kernel (ajx_scan_fused) for multi-tenant batches and on
-    // ablate 40; 1..3 / 10..12 its profiling variants
-    bool fast_tables = !force_scan;
-    for (uint32_t i = 0; i < n_sets && fast_tables; i++)
-        fast_tables = (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagFastOk) != 0;
+    // kernel: the lean single-pass kernel (ajx_lean.h; ablate 40: the token scanner of
+    // ajx_fast.h), the exact scan for what it hands over
     bool mods = false;  // modifier chains: the exact scan's instance with text buffers
     for (uint32_t i = 0; i < n_sets; i++)
         mods = mods || reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->n_modifiers != 0 ||
                (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagBufs) != 0;
-    // the row kernel (ajx_row.h; default for a batch over one ruleset with row tables);
-    // ablate 40 keeps the token-scanner single-pass kernel, 41 is the row scan alone
-    const ajx::RulesetHdr* h0 = reinterpret_cast<const ajx::RulesetHdr*>(sets[0]->c.blob.data());
-    const bool row = fast_tables && n_sets == 1 && (ablate == 0 || (ablate >= 41 && ablate <= 44)) && h0->off_row != 0 &&
-                     h0->n_selectors <= 64 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes &&
-                     ajx::row_kernel_fits((uint32_t)sets[0]->c.blob.size());
     // capture rows kept for authjx_select_from_eval_device: one ruleset, a full kernel
     const bool full = ablate == 0 || ablate == 40 || (ablate >= 10 && ablate <= 12);
     const bool keep_rows = !force_scan && n_sets == 1 && full;
@@ -418,28 +398,15 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
             perm = w->d_perm;
         }
         w->rows_perm = perm;
-        if (row) {
-            // the row kernel decides in-kernel; it writes capture rows (one per request)
-            // only for a forest, whose selector tree authjx_select_from_eval_device reads
-            const bool rows = keep_rows && sets[0]->c.n_trees > 1;
-            if (!rows) w->rows_rs = nullptr;
-            w->rows_perm = nullptr;
-            w->rows_wave = false;
-            HIP_OK(ajx::launch_eval_row(w->d_sets, (uint32_t)sets[0]->c.blob.size(), h0->n_selectors, d_arena, d_offs,
-                                        d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
-                                        rows ? w->d_rows : nullptr, row_stride, w->d_slow, w->d_tier, s, perm, mods,
-                                        ablate));
-        } else {
-            // uniform batch: the blob staged once per workgroup; multi-tenant batch: nonzero
-            // turns on the per-workgroup staging of its runs' rulesets (ajx_scan_fused_tenant)
-            const uint32_t stage_bytes =
-                n_sets == 1 ? (max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u)
-                            : (!no_tenant_stage ? (uint32_t)std::min<size_t>(max_blob, ajx::kMaxTenantStageBytes) : 0u);
-            HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
-                                         d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
-                                         w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
-                                         ablate < 20 ? ablate : 0, perm, mods));
-        }
+        // uniform batch: the blob staged once per workgroup; multi-tenant batch: nonzero
+        // turns on the per-workgroup staging of its runs' rulesets (ajx_scan_fused_tenant)
+        const uint32_t stage_bytes =
+            n_sets == 1 ? (max_blob <= ajx::kMaxSharedBlobBytes ? (uint32_t)max_blob : 0u)
+                        : (!no_tenant_stage ? (uint32_t)std::min<size_t>(max_blob, ajx::kMaxTenantStageBytes) : 0u);
+        HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
+                                     d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
+                                     w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
+                                     (ablate < 20 || ablate == 40) ? ablate : 0, perm, mods));
     }
     return batch_done(w, sets, n_sets);
 }

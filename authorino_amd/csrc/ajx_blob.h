@@ -160,12 +160,18 @@ constexpr uint32_t kEmptySlot = 0xFFFFFFFFu;
 constexpr uint32_t kMaxKeySlotsLog2 = 9;
 constexpr uint32_t kKeyProbes = 4;  // the table is grown until every key is this close to home
 
-AJX_BLOB_HD inline uint32_t key_slot_hash(uint64_t sig, uint32_t klen, uint32_t parent, uint32_t log2) {
+// (mult: an odd multiplier the compiler picks per ruleset, so that keys sit in their home
+// slots; key_mult in the header)
+AJX_BLOB_HD inline uint32_t key_slot_hash(uint64_t sig, uint32_t klen, uint32_t parent, uint32_t log2,
+                                          uint32_t mult) {
     uint32_t x = (uint32_t)sig ^ (((uint32_t)(sig >> 32) << 13) | ((uint32_t)(sig >> 32) >> 19)) ^ (klen << 24) ^
                  (parent << 16);
-    x *= 0x9E3779B1u;
+    x *= mult;
     return x >> (32 - log2);
 }
+// the key-length field of a key-table entry that is an array index (sig = the index): the
+// lean scan looks up array elements in the same table (keys that long go to the exact scan)
+constexpr uint32_t kIndexKeyLen = 0xFFFFu;
 
 struct SelectorPatterns {
     uint32_t begin;        // index into the uint16 pattern list
@@ -201,8 +207,7 @@ struct RulesetHdr {
     uint32_t hot_bytes;         // [0, hot_bytes): every table the single-pass kernels read
                                 // (selectors, components, modifiers follow: exact scan only)
     uint32_t key_probes;        // every key sits within key_probes slots of its home slot
-    uint32_t off_row;           // RowHdr of the row kernel's tables (0: none, that kernel
-                                // does not take this ruleset)
+    uint32_t key_mult;          // key_slot_hash multiplier
     uint32_t pad2[3];
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
@@ -210,38 +215,6 @@ struct RulesetHdr {
 };
 constexpr uint32_t kFlagFastOk = 4;
 
-// ---- row kernel (ajx_row.h): key dictionary + transition table -------------------
-// Every distinct key of the trie's edges gets a key id (kid); a document key is looked
-// up once, by its text alone, in the key dictionary (open addressing on the key's last
-// <= 8 bytes and its length; longer keys then compare the rest with the literal pool),
-// and the trie step is trans[node][kid].
-struct RowHdr {
-    uint32_t off_nodes;   // u32 per trie node: leaf selector + 1 (bits 0..7), bit 8 index edges
-    uint32_t n_nodes;
-    uint32_t off_trans;   // u8 [n_nodes][n_kids], 0xFF none
-    uint32_t n_kids;
-    uint32_t off_kdict;   // KeyDictSlot[1 << kd_log2]
-    uint32_t kd_log2;
-    uint32_t kd_probes;   // every key within kd_probes slots of its home slot
-    uint32_t off_idx;     // u32 per array-index edge: parent | child << 8 | index << 16
-    uint32_t n_idx;
-    uint32_t pad[3];
-};
-struct KeyDictSlot {
-    uint32_t sig_lo, sig_hi;  // key_signature
-    uint32_t meta;            // len (bits 0..15) | kid << 16; 0xFFFFFFFF empty
-    uint32_t key_off;         // key bytes in the literal pool (4-byte aligned)
-};
-static_assert(sizeof(KeyDictSlot) == 16, "KeyDictSlot layout");
-constexpr uint32_t kRowMaxKids = 250;     // kids 0xFE / 0xFF: escaped key / no key
-constexpr uint32_t kRowMaxDictLog2 = 12;
-constexpr uint32_t kRowDictProbes = 4;
-AJX_BLOB_HD inline uint32_t kdict_slot(uint64_t sig, uint32_t len, uint32_t log2) {
-    const uint32_t lo = (uint32_t)sig, hi = (uint32_t)(sig >> 32);
-    uint32_t x = lo ^ ((hi << 13) | (hi >> 19)) ^ (len << 24);
-    x *= 0x9E3779B1u;
-    return log2 ? x >> (32 - log2) : 0u;
-}
 constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the exact scan's buffers
 
 }  // namespace ajx

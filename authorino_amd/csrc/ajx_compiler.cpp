@@ -658,7 +658,6 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
 
     // ---- assemble ----
     Builder b;
-    uint32_t hdr_row_off = 0;
     RulesetHdr hdr;
     std::memset(&hdr, 0, sizeof hdr);
     b.append(&hdr, sizeof hdr);
@@ -687,31 +686,57 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 tc.push_back(ch);
             }
         }
-        // key table (linear probing): load factor <= 1/2, then grown until every key sits
-        // within kKeyProbes slots of its home slot (up to kMaxKeySlotsLog2); key_probes, the
-        // largest distance, bounds every lookup's probe sequence (a wave runs its longest
-        // lane's sequence: a miss no longer walks to the end of its cluster)
-        uint32_t log2 = 4;
-        while ((1u << log2) < 2 * tc.size() && log2 < kMaxKeySlotsLog2) log2++;
-        std::vector<KeySlot> slots;
-        uint32_t probes = 1;
-        for (;;) {
-            slots.assign(1u << log2, KeySlot{0, kEmptySlot, 0});
-            probes = 1;
-            for (size_t i = 0; i < trie.size(); i++) {
-                for (uint32_t j = 0; j < tn[i].n_children; j++) {
-                    const TrieChild& ch = tc[tn[i].child_begin + j];
-                    uint32_t at = key_slot_hash(ch.sig, ch.key_len, (uint32_t)i, log2), dist = 1;
-                    while (slots[at].meta != kEmptySlot) at = (at + 1) & ((1u << log2) - 1), dist++;
-                    slots[at].sig = ch.sig;
-                    slots[at].meta = ch.key_len | ((uint32_t)i << 16) | (ch.node << 24);
-                    slots[at].key_off = ch.key_off;
-                    probes = std::max(probes, dist);
-                }
+        // key table (linear probing): every (parent, key) edge, and every (parent, array
+        // index) edge as an entry of length kIndexKeyLen. Sizes from load 1/2 up to
+        // kMaxKeySlotsLog2, and per size a search over hash multipliers for a table where
+        // every entry sits in its home slot (key_probes 1: a lookup is one slot read); else
+        // the smallest largest distance found (key_probes bounds every lookup's probes)
+        struct Ent {
+            uint64_t sig;
+            uint32_t len, parent, node, key_off;
+        };
+        std::vector<Ent> ents;
+        for (size_t i = 0; i < trie.size(); i++)
+            for (uint32_t j = 0; j < tn[i].n_children; j++) {
+                const TrieChild& ch = tc[tn[i].child_begin + j];
+                if (ch.key_len < kIndexKeyLen) ents.push_back({ch.sig, ch.key_len, (uint32_t)i, ch.node, ch.key_off});
+                if (ch.array_index >= 0)
+                    ents.push_back({(uint64_t)(uint32_t)ch.array_index, kIndexKeyLen, (uint32_t)i, ch.node, 0});
             }
-            if (probes <= kKeyProbes || log2 >= kMaxKeySlotsLog2) break;
-            log2++;
+        uint32_t log2 = 4;
+        while ((1u << log2) < 2 * ents.size() && log2 < kMaxKeySlotsLog2) log2++;
+        std::vector<KeySlot> slots, best_slots;
+        uint32_t probes = 0xFFFFFFFFu, best_log2 = log2, mult = 0x9E3779B1u;
+        auto build = [&](uint32_t lg, uint32_t m, std::vector<KeySlot>& out) -> uint32_t {
+            out.assign(1u << lg, KeySlot{0, kEmptySlot, 0});
+            uint32_t worst = 1;
+            for (const Ent& e : ents) {
+                uint32_t at = key_slot_hash(e.sig, e.len, e.parent, lg, m), dist = 1;
+                while (out[at].meta != kEmptySlot) at = (at + 1) & ((1u << lg) - 1), dist++;
+                out[at].sig = e.sig;
+                out[at].meta = e.len | (e.parent << 16) | (e.node << 24);
+                out[at].key_off = e.key_off;
+                worst = std::max(worst, dist);
+            }
+            return worst;
+        };
+        for (uint32_t lg = log2; lg <= kMaxKeySlotsLog2 && probes > 1; lg++) {
+            uint32_t m = 0x9E3779B1u;
+            for (int t = 0; t < 512 && probes > 1; t++) {
+                const uint32_t worst = build(lg, m, slots);
+                if (worst < probes) {
+                    probes = worst;
+                    best_log2 = lg;
+                    mult = m;
+                    best_slots = slots;
+                }
+                m = m * 0x2C1B3C6Du + 0x297A2D38u;  // next candidate (odd)
+                m |= 1u;
+            }
         }
+        log2 = best_log2;
+        slots = best_slots;
+        hdr.key_mult = mult;
         hdr.key_slots_log2 = log2;
         hdr.key_probes = probes;
         hdr.n_trie_nodes = (uint32_t)tn.size();
@@ -721,86 +746,6 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         b.append(tc.data(), tc.size() * sizeof(TrieChild));
         hdr.off_key_slots = (uint32_t)b.align16();
         b.append(slots.data(), slots.size() * sizeof(KeySlot));
-        // row kernel tables: key ids, transition table, key dictionary, index edges
-        // (kept before hot_bytes: every table a single-pass kernel reads)
-        if (fast_ok) {
-            std::map<std::string, uint32_t> kid_of;
-            std::vector<std::string> kid_keys;
-            bool row_ok = true;
-            std::vector<uint32_t> idx_edges;
-            for (size_t i = 0; i < trie.size(); i++)
-                for (size_t j = 0; j < trie[i].kids.size(); j++) {
-                    const std::string& key = trie[i].keys[j].first;
-                    if (!kid_of.count(key)) {
-                        kid_of[key] = (uint32_t)kid_keys.size();
-                        kid_keys.push_back(key);
-                    }
-                    const int32_t ai = trie[i].keys[j].second;
-                    if (ai >= 0) {
-                        if (ai > 0xFFFF) row_ok = false;
-                        idx_edges.push_back((uint32_t)i | (trie[i].kids[j] << 8) | ((uint32_t)ai << 16));
-                    }
-                    if (key.size() > 0xFFFF) row_ok = false;
-                }
-            if (kid_keys.size() > kRowMaxKids) row_ok = false;
-            const uint32_t nk = (uint32_t)std::max<size_t>(kid_keys.size(), 1);
-            if ((uint64_t)trie.size() * nk > 64 * 1024) row_ok = false;
-            // dictionary: load <= 1/2, grown until every key is within kRowDictProbes of home
-            uint32_t dlog2 = 2, dprobes = 1;
-            std::vector<KeyDictSlot> dict;
-            std::vector<uint32_t> key_off(kid_keys.size());
-            for (size_t k = 0; k < kid_keys.size(); k++) {
-                while (lits.size() % 4) lits.push_back('\0');
-                key_off[k] = (uint32_t)lits.size();
-                lits += kid_keys[k];
-            }
-            while (row_ok) {
-                while ((1u << dlog2) < 2 * kid_keys.size()) dlog2++;
-                dict.assign(1u << dlog2, KeyDictSlot{0, 0, 0xFFFFFFFFu, 0});
-                dprobes = 1;
-                for (size_t k = 0; k < kid_keys.size(); k++) {
-                    const std::string& key = kid_keys[k];
-                    const uint64_t sig = key_signature((const uint8_t*)key.data(), (uint32_t)key.size());
-                    uint32_t at = kdict_slot(sig, (uint32_t)key.size(), dlog2), dist = 1;
-                    while (dict[at].meta != 0xFFFFFFFFu) at = (at + 1) & ((1u << dlog2) - 1), dist++;
-                    dict[at] = KeyDictSlot{(uint32_t)sig, (uint32_t)(sig >> 32),
-                                           (uint32_t)key.size() | ((uint32_t)k << 16), key_off[k]};
-                    dprobes = std::max(dprobes, dist);
-                }
-                if (dprobes <= kRowDictProbes) break;
-                if (dlog2 >= kRowMaxDictLog2) { row_ok = false; break; }
-                dlog2++;
-            }
-            if (row_ok) {
-                std::vector<uint32_t> nodes(trie.size(), 0);
-                std::vector<uint8_t> trans(trie.size() * nk, 0xFF);
-                for (size_t i = 0; i < trie.size(); i++) {
-                    nodes[i] = trie[i].selector >= 0 ? (uint32_t)trie[i].selector + 1u : 0u;
-                    for (size_t j = 0; j < trie[i].kids.size(); j++) {
-                        trans[i * nk + kid_of[trie[i].keys[j].first]] = (uint8_t)trie[i].kids[j];
-                        if (trie[i].keys[j].second >= 0) nodes[i] |= 1u << 8;
-                    }
-                }
-                RowHdr rh;
-                std::memset(&rh, 0, sizeof rh);
-                hdr_row_off = (uint32_t)b.align16();
-                b.append(&rh, sizeof rh);
-                rh.off_nodes = (uint32_t)b.align16();
-                b.append(nodes.data(), nodes.size() * 4);
-                rh.n_nodes = (uint32_t)nodes.size();
-                rh.off_trans = (uint32_t)b.align16();
-                b.append(trans.data(), trans.size());
-                rh.n_kids = (uint32_t)kid_keys.size();
-                rh.off_kdict = (uint32_t)b.align16();
-                b.append(dict.data(), dict.size() * sizeof(KeyDictSlot));
-                rh.kd_log2 = dlog2;
-                rh.kd_probes = dprobes;
-                rh.off_idx = (uint32_t)b.align16();
-                b.append(idx_edges.data(), idx_edges.size() * 4);
-                rh.n_idx = (uint32_t)idx_edges.size();
-                std::memcpy(b.blob.data() + hdr_row_off, &rh, sizeof rh);
-            }
-        }
         std::vector<SelectorPatterns> sp(sels.size());
         std::vector<uint16_t> plist;
         for (size_t s = 0; s < sels.size(); s++) {
@@ -879,7 +824,6 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     hdr.lit_bytes = (uint32_t)lits.size();
     hdr.n_components = (uint32_t)comps.size();
     hdr.flags = flags;
-    hdr.off_row = hdr_row_off;
     std::memcpy(b.blob.data(), &hdr, sizeof hdr);
     out->blob = std::move(b.blob);
     out->n_patterns = np;

@@ -145,6 +145,7 @@ struct Scan {
     const TrieChild* tc;
     const KeySlot* ks;  // key table (1 << (ks_meta & 0xFF) slots)
     uint32_t ks_meta;   // log2 of the slot count | key_probes << 8 (one register for both)
+    uint32_t ks_mult;   // key_slot_hash multiplier
     const uint8_t* lits;
     const uint8_t* d;
     RowRef row;     // capture row (header + records)
@@ -384,9 +385,9 @@ struct Scan {
         uint64_t sig = tail8(i);
         if (klen < 8) sig = klen ? sig >> (8 * (8 - klen)) : 0ull;
 #endif
-        if (klen > 0xFFFFu) return;
+        if (klen >= kIndexKeyLen) return;
         const uint32_t log2 = ks_meta & 0xFFu, want = klen | (parent << 16), mask = (1u << log2) - 1u;
-        const uint32_t at = key_slot_hash(sig, klen, parent, log2);
+        const uint32_t at = key_slot_hash(sig, klen, parent, log2, ks_mult);
 #ifdef AJX_KEY_UNROLL  // (experiment: the key_probes <= 4 slots read at once, no loop)
         if ((ks_meta >> 8) <= kKeyProbes) {
             uint32_t cand = 0, node = kNoNode, koff = 0;
@@ -671,6 +672,7 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     s.tc = tab.tc;
     s.ks = tab.ks;
     s.ks_meta = h->key_slots_log2 | h->key_probes << 8;
+    s.ks_mult = h->key_mult;
     s.lits = blob + h->off_literals;
     s.d = d;
     s.row = row;

@@ -51,27 +51,6 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
                             int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false);
 
-// The row kernel (ajx_row.h, one ruleset for the whole batch, blob with row tables):
-// capture rows for every request (d_rows, row_stride u64 each, one per request), then
-// stage B, then the exact scan of what it handed over. d_slow: [0] count + n ids;
-// d_tier: 2 x (n + 1) u32 of tier lists. mode 41 (profiling): the row scan only.
-hipError_t launch_eval_row(const uint8_t* const* d_sets, uint32_t blob_bytes, uint32_t n_selectors,
-                           const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
-                           uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
-                           uint32_t row_stride, uint32_t* d_slow, uint32_t* d_tier, hipStream_t stream,
-                           const uint32_t* d_perm, bool mods, int mode);
-
-// The row kernel's LDS (ruleset blob + every tier's row buffers) fits a workgroup.
-bool row_kernel_fits(uint32_t blob_bytes);
-
-// The row kernel (ajx_rowk.hip): the tiers' launches, stage B included; d_rows (may be
-// null) receives the capture rows.
-hipError_t launch_row_scan(const uint8_t* const* d_sets, uint32_t blob_bytes, const uint8_t* d_arena,
-                           const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint64_t* d_rows,
-                           uint32_t row_stride, uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride,
-                           uint32_t* d_slow, uint32_t* d_tier, hipStream_t stream, const uint32_t* d_perm,
-                           uint32_t stop = 0);
-
 // Length-bucketed request order for the single-pass kernel: d_perm[n] = request ids,
 // longest 8-byte length class first; d_hist needs 2 * 1024 + 1 u32 of scratch.
 hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist, uint32_t* d_perm,

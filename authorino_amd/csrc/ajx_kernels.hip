@@ -14,6 +14,7 @@
 #include <atomic>
 
 #include "ajx_fast.h"
+#include "ajx_lean.h"
 #include "ajx_modifiers.h"
 #include "ajx_kernels.h"
 
@@ -371,6 +372,66 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
     }
 }
 
+// The lean single-pass kernel (ajx_lean.h): stage A with the lean scan, then stage B in the
+// same work-item. Dynamic LDS: [blob copy (SHARED)] [per wave: 64 lanes x 144-B rings].
+constexpr uint32_t kLeanRingBytesPerWave = 64 * lean::kRingStride;
+template <bool SHARED>
+__global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_lean(
+    const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
+    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
+    uint64_t* __restrict__ rows, uint32_t row_stride, uint32_t* __restrict__ slow_count,
+    uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+    uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t ring_off, const uint32_t* __restrict__ perm) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t r = k < n ? (perm ? perm[k] : k) : 0u;
+    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : set_of_req[r]]);
+    if (k >= n) return;
+    extern __shared__ uint4 s_lean_dyn[];
+    uint8_t* ring = reinterpret_cast<uint8_t*>(s_lean_dyn) + ring_off + threadIdx.x * lean::kRingStride;
+    const RowRef row = wave_row(rows, row_stride, k);
+    const uint8_t* d = arena + offs[r];
+    const uint32_t len = lens[r];
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    bool ok = (h->flags & kFlagFastOk) && len < (1u << 24);
+    if (ok) {
+        const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
+        auto load = [&](uint32_t b, uint32_t nblk) -> Block16 {
+            if (b < nblk) {
+                const uint4 v = a4[b];
+                return Block16{v.x, v.y, v.z, v.w};
+            }
+            return Block16{0u, 0u, 0u, 0u};
+        };
+        ok = lean::scan_doc(blob, blob_tables(blob), d, len, row, ring, load);
+    } else {
+        row[0] = kRowSlow;
+    }
+    if (!ok) {
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
+        return;
+    }
+#ifdef AJX_ABLATE_FUSED_NOB  // profiling: stage A alone (outputs meaningless)
+    out_tri[r] = (uint8_t)row[0];
+    return;
+#endif
+    if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
+        row[0] = kRowSlow;
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
+    }
+}
+// workgroup size for the lean kernel with a staged blob of `blob_bytes` (as fast_block)
+static uint32_t lean_block(uint32_t blob_bytes) {
+    const uint32_t stage = (blob_bytes + 15u) & ~15u;
+    uint32_t best = 0, best_w = 0;
+    for (uint32_t b = 256; b <= kFastMaxBlock; b *= 2) {
+        const uint32_t lds = stage + (b / 64) * kLeanRingBytesPerWave;
+        uint32_t w = lds <= 160u * 1024u ? (160u * 1024u / lds) * (b / 64) : 0u;
+        if (w > 4u * AJX_FAST_WAVES) w = 4u * AJX_FAST_WAVES;
+        if (w > best_w) best = b, best_w = w;
+    }
+    return best ? best : 256u;
+}
+
 // The single-pass kernel for multi-tenant batches (one ruleset per request through
 // set_of_req; the caller buckets requests by AuthConfig, so a workgroup's requests form a
 // few runs of one ruleset each). The workgroup finds its runs (a run starts where the
@@ -708,7 +769,9 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             reinterpret_cast<const void*>(&ajx_scan_fast<1, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<2, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fused<true>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused<false>)};
+                            reinterpret_cast<const void*>(&ajx_scan_fused<false>),
+                            reinterpret_cast<const void*>(&ajx_scan_lean<true>),
+                            reinterpret_cast<const void*>(&ajx_scan_lean<false>)};
         for (const void* k : ks) {
             const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (r != hipSuccess) return r;
@@ -747,7 +810,19 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
             hipLaunchKernelGGL((ajx_patterns<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
         }
-    } else if (shared) {  // the single-pass kernel (token scanner)
+    } else if (mode != 40 && !(d_set_of_req && !shared)) {  // the lean single-pass kernel (default)
+        const uint32_t lblock = shared ? lean_block(shared_blob_bytes) : 256u;
+        const uint32_t lgrid = (n + lblock - 1) / lblock;
+        const uint32_t llds = ring_off + (lblock / 64) * kLeanRingBytesPerWave;
+        if (shared)
+            hipLaunchKernelGGL((ajx_scan_lean<true>), dim3(lgrid), dim3(lblock), llds, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
+                               d_bm, stride, ring_off, d_perm);
+        else
+            hipLaunchKernelGGL((ajx_scan_lean<false>), dim3(lgrid), dim3(lblock), llds, stream, d_sets, d_set_of_req,
+                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
+                               d_bm, stride, ring_off, d_perm);
+    } else if (shared) {  // the token-scanner single-pass kernel (kernel mode 40)
         hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
                            d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride,
                            ring_off, d_perm);
@@ -771,28 +846,6 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
     const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
     launch_slow_list(mods, sgrid, stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids,
                      d_tri, d_err, d_bm, stride);
-    return hipGetLastError();
-}
-
-// The row kernel's tiers (ajx_rowk.hip), then the exact scan of the requests they handed
-// over. Profiling modes: 41 the tiers alone; 42 / 43 / 44 stop the tiers after the
-// classification / the structure pass / row_finish (outputs meaningless).
-hipError_t launch_eval_row(const uint8_t* const* d_sets, uint32_t blob_bytes, uint32_t n_selectors,
-                           const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
-                           uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
-                           uint32_t row_stride, uint32_t* d_slow, uint32_t* d_tier, hipStream_t stream,
-                           const uint32_t* d_perm, bool mods, int mode) {
-    if (n == 0) return hipSuccess;
-    if ((d_rows && row_stride < 1 + n_selectors) || n_selectors > 64u) return hipErrorInvalidValue;
-    const uint32_t stop = mode >= 42 && mode <= 44 ? (uint32_t)(mode - 41) : 0u;
-    hipError_t e = launch_row_scan(d_sets, blob_bytes, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_tri, d_err,
-                                   d_bm, stride, d_slow, d_tier, stream, d_perm, stop);
-    if (e != hipSuccess) return e;
-    if (mode >= 41 && mode <= 44) return hipSuccess;
-    const uint32_t grid = (n + 255u) / 256u;
-    const uint32_t sgrid = grid < 2048 ? 2 * grid : 4096;
-    launch_slow_list(mods, sgrid, stream, d_sets, nullptr, d_arena, d_offs, d_lens, d_slow, d_slow + 1, d_tri, d_err,
-                     d_bm, stride);
     return hipGetLastError();
 }
 

@@ -143,6 +143,54 @@ __global__ __launch_bounds__(256) void varE(const uint8_t* arena, const uint64_t
     out[r] = acc;
 }
 
+
+// F: per-lane 128-B windows landed in LDS by LDS-DMA (global_load_lds_dwordx4; no VGPRs
+// hold the data), two windows per lane (the next one in flight while the current one is
+// read back with ds_read_b128). Chunk-major ring: chunk j of slot s of lane l at
+// ((s * 8 + j) * 64 + l) * 16 inside the wave's region.
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void varF(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
+                                                 uint32_t n, uint32_t* out) {
+    extern __shared__ uint4 sm[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint4* wr = sm + wv * (2 * 8 * 64);
+    typedef __attribute__((address_space(3))) uint8_t lds8;
+    lds8* wl = (lds8*)(uint8_t*)wr;
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t rr = r < n ? r : n - 1;
+    const uint8_t* d = arena + offs[rr];
+    const uint32_t len = r < n ? lens[rr] : 0;
+    const uint32_t mis = (uint32_t)((uintptr_t)d & 15u);
+    const uint8_t* a = d - mis;
+    const uint32_t nblk = (len + mis + 15) / 16;
+    uint32_t wmax = (nblk + 7) / 8;
+    for (int o = 32; o; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o));
+    uint32_t acc = 0;
+    auto issue = [&](uint32_t w, uint32_t slot) {
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t b = w * 8 + j;
+            const uint8_t* src = a + 16 * (b < nblk ? b : 0);
+            __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(wl + (slot * 8 + j) * 1024), 16, 0, 0);
+        }
+    };
+    issue(0, 0);
+    for (uint32_t w = 0; w < wmax; w++) {
+        if (w + 1 < wmax) {
+            issue(w + 1, (w + 1) & 1);
+            __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): this window landed
+        } else {
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint4 v = wr[((w & 1) * 8 + j) * 64 + lane];
+            acc ^= v.x + v.y * 3 + v.z * 5 + v.w * 7;
+        }
+    }
+    if (r < n) out[r] = acc;
+}
+
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? atoi(argv[1]) : (1u << 20);
     std::mt19937 g(2);
@@ -167,9 +215,10 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char* names[5] = {"A_lane64B", "B_lane128B", "C_coop_lds", "D_coalesced", "E_lane128B_2ahead"};
+    const char* names[7] = {"A_lane64B", "B_lane128B", "C_coop_lds", "D_coalesced", "E_lane128B_2ahead", "F_dma128B_wpb4", "F_dma128B_wpb2"};
+    CK(hipFuncSetAttribute((const void*)varF<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
     for (int rep = 0; rep < 3; rep++)
-        for (int v = 0; v < 5; v++) {
+        for (int v = 0; v < 7; v++) {
             CK(hipEventRecord(e0));
             for (int it = 0; it < 10; it++) {
                 if (v == 0) varA<<<(n + 255) / 256, 256>>>(da, doffs, dlens, n, dout);
@@ -177,6 +226,8 @@ int main(int argc, char** argv) {
                 if (v == 2) varC<<<(n + 255) / 256, 256>>>(da, doffs, dlens, n, dout);
                 if (v == 3) varD<<<4096, 256>>>((const uint4*)da, tot / 16, dout);
                 if (v == 4) varE<<<(n + 255) / 256, 256>>>(da, doffs, dlens, n, dout);
+                if (v == 5) varF<4><<<(n + 255) / 256, 256, 65536>>>(da, doffs, dlens, n, dout);
+                if (v == 6) varF<2><<<(n + 127) / 128, 128, 32768>>>(da, doffs, dlens, n, dout);
             }
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));

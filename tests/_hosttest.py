@@ -171,43 +171,35 @@ def eval_tok(hr: "HostRuleset", doc, mis: int = 0, n_sel: int = 0):
     return t, err.value, list(res)[: hr.n], (list(row)[: 1 + n_sel] if t >= 0 else None)
 
 
-def _row_decl():
+
+
+def _lean_decl():
     L = lib()
-    if not hasattr(L, "_row_declared"):
-        L.rt_scan.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
-                              C.c_uint32, C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32]
-        L.rt_scan.restype = C.c_int
-        L.rt_eval.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8),
-                              C.POINTER(C.c_int32), C.c_uint32, C.c_uint32]
-        L.rt_eval.restype = C.c_int
-        L._row_declared = True
+    if not hasattr(L, "_lean_declared"):
+        L.ht_eval_lean_row.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8),
+                                       C.POINTER(C.c_int32), C.c_void_p]
+        L.ht_eval_lean_row.restype = C.c_int
+        L.ht_lean_classes.argtypes = [C.c_char_p, C.POINTER(C.c_uint32)]
+        L.ht_lean_classes.restype = None
+        L._lean_declared = True
     return L
 
 
-ROW_MAXB, ROW_MAXE = 8192, 2048
-
-
-def eval_row(hr: "HostRuleset", doc, mis: int = 0, maxb: int = ROW_MAXB, maxe: int = ROW_MAXE):
-    """The row kernel (64-lane host emulation) + stage B: (tri | -1 exact scan | -2 no row
-    tables, err, res)."""
-    L = _row_decl()
+def eval_lean(hr: "HostRuleset", doc, mis: int = 0, n_sel: int = 0):
+    """The lean single-pass scan (ajx_lean.h) + stage B on the host: (tri | -1 exact scan |
+    -2 not eligible, err, res, capture row or None)."""
+    L = _lean_decl()
     d = _b(doc)
     res = (C.c_uint8 * max(hr.n, 1))()
     err = C.c_int32(-1)
-    t = L.rt_eval(hr._h, d, len(d), mis, res, C.byref(err), maxb, maxe)
-    return t, err.value, list(res)[: hr.n]
+    row = (C.c_uint64 * (1 + max(n_sel, 64)))()
+    t = L.ht_eval_lean_row(hr._h, d, len(d), mis, res, C.byref(err), C.cast(row, C.c_void_p))
+    return t, err.value, list(res)[: hr.n], (list(row)[: 1 + n_sel] if t >= 0 else None)
 
 
-def scan_rows(hr: "HostRuleset", docs, mis, n_sel: int, maxb: int = ROW_MAXB, maxe: int = ROW_MAXE):
-    """Up to four documents as one wavefront of the row kernel: their capture rows
-    (header kRowSlow = exact scan)."""
-    L = _row_decl()
-    nd = len(docs)
-    bs = [_b(x) for x in docs]
-    arr = (C.c_char_p * 4)(*(bs + [b""] * (4 - nd)))
-    lens = (C.c_uint32 * 4)(*([len(x) for x in bs] + [0] * (4 - nd)))
-    ms = (C.c_uint32 * 4)(*(list(mis) + [0] * (4 - nd)))
-    rows = (C.c_uint64 * (4 * (1 + n_sel)))()
-    rc = L.rt_scan(hr._h, arr, lens, ms, nd, rows, maxb, maxe)
-    out = list(rows)
-    return rc, [out[k * (1 + n_sel):(k + 1) * (1 + n_sel)] for k in range(nd)]
+def lean_classes(b32: bytes):
+    """The lean scan's eight byte-class masks of 32 bytes (LUT + transpose)."""
+    L = _lean_decl()
+    out = (C.c_uint32 * 8)()
+    L.ht_lean_classes(bytes(b32), out)
+    return list(out)

@@ -9,6 +9,7 @@
 
 #include "../../authorino_amd/csrc/ajx_compiler.h"
 #include "../../authorino_amd/csrc/ajx_fast.h"
+#include "../../authorino_amd/csrc/ajx_lean.h"
 #include "../../authorino_amd/csrc/ajx_modifiers.h"
 #include "../../authorino_amd/csrc/ajx_regex.h"
 
@@ -221,151 +222,54 @@ static int eval_single_pass(void* h, const uint8_t* doc, uint32_t len, uint32_t 
 
 extern "C" uint32_t ht_blob_size(void* h) { return (uint32_t)((HtRuleset*)h)->c.blob.size(); }
 
+
+
 // ---------------------------------------------------------------------------------
-// The row kernel (ajx_row.h) on the 64-lane host emulation (ajx_wave.h): up to four
-// documents as one wavefront's rows. rows_out: 4 x (1 + n_selectors) capture rows
-// (header kRowSlow when the document goes to the exact scan). Returns the number of
-// rows accepted, or -2 when the ruleset has no row tables.
-#include "../../authorino_amd/csrc/ajx_row.h"
-extern "C" int rt_scan(void* h, const uint8_t* const* docs, const uint32_t* lens, const uint32_t* mis_in, uint32_t nd,
-                       uint64_t* rows_out, uint32_t maxb, uint32_t maxe) {
-    using namespace ajx::w;
-    std::vector<uint8_t> blobv = ((HtRuleset*)h)->c.blob;
-    const uint8_t* gblob = blobv.data();
-    const RulesetHdr* hd = (const RulesetHdr*)gblob;
-    if (!(hd->flags & kFlagFastOk) || hd->off_row == 0) return -2;
-    const RowLayout L = row_layout(maxb, maxe);
-    std::vector<uint8_t> lds(L.bytes + 64, 0xA5);
-    const RowTabs T = row_tabs(gblob, blobv.data());
-    // each document in its own buffer at the requested misalignment (slack around it)
-    std::vector<std::vector<uint8_t>> bufs(4);
-    const uint8_t* bases[4] = {nullptr, nullptr, nullptr, nullptr};
-    V len(0u), mis(0u);
-    M live(false);
-    for (uint32_t r = 0; r < 4; r++) {
-        bufs[r].assign((r < nd ? lens[r] : 0) + 64, 0x5A);
-        uintptr_t a = ((uintptr_t)bufs[r].data() + 15) & ~(uintptr_t)15;
-        const uint32_t m = r < nd ? (mis_in[r] & 15u) : 0u;
-        if (r < nd && lens[r]) std::memcpy((uint8_t*)a + m, docs[r], lens[r]);
-        bases[r] = (const uint8_t*)a;
-        for (int l = 0; l < 16; l++) {
-            len.x[16 * r + l] = r < nd ? lens[r] : 0u;
-            mis.x[16 * r + l] = m;
-            if (r < nd) live.b |= 1ull << (16 * r + l);
-        }
-    }
-    auto load = [&](const V& b, const M& m) -> G16 {
-        P a;
-        for (int l = 0; l < 64; l++) a.p[l] = m.at(l) ? bases[l >> 4] + 16u * b.x[l] : nullptr;
-        return gld128(a, m);
-    };
-    const uint32_t ns = hd->n_selectors;
-    M ok = row_scan(T, lds.data(), L, live, len, mis, load);
-    std::vector<uint64_t> recs(4 * (size_t)(1 + ns), 0);
-    V hlo, hhi;
-    ok = row_finish(T, lds.data(), L, ok, mis, hlo, hhi,
-                    [&](const V& s, const M& m, const M& found, const V& start, const V& ln, const V& type, const V& esc) {
-                        for (int l = 0; l < 64; l++) {
-                            if (!m.at(l)) continue;
-                            const uint32_t r = l >> 4;
-                            const uint64_t rec = found.at(l) ? ((uint64_t)start.x[l] |
-                                                                ((uint64_t)((ln.x[l] & 0xFFFFFFu) | (type.x[l] << 24) |
-                                                                            (esc.x[l] << 27)) << 32))
-                                                             : 0ull;
-                            if (found.at(l)) recs[r * (1 + ns) + 1 + s.x[l]] = rec;
-                        }
-                    });
-    int acc = 0;
-    for (uint32_t r = 0; r < nd; r++) {
-        uint64_t* ro = rows_out + (size_t)r * (1 + ns);
-        if (!ok.at(16 * r)) {
-            ro[0] = kRowSlow;
-            continue;
-        }
-        acc++;
-        ro[0] = (uint64_t)hlo.x[16 * r] | ((uint64_t)hhi.x[16 * r] << 32);
-        for (uint32_t s = 0; s < ns; s++) ro[1 + s] = recs[r * (1 + ns) + 1 + s];
-    }
-    return acc;
-}
-
-// the whole row kernel (row scan + in-kernel stage B) for up to four documents:
-// tri[d * n_trees + k], err[...], bm[d * bm_words + w]; returns a bit per document that
-// stayed on the row path (the others belong to the exact scan).
-extern "C" int rt_run(void* h, const uint8_t* const* docs, const uint32_t* lens, const uint32_t* mis_in, uint32_t nd,
-                      uint8_t* tri, int32_t* err, uint64_t* bm, uint32_t bm_words, uint32_t maxb, uint32_t maxe) {
-    using namespace ajx::w;
-    std::vector<uint8_t> blobv = ((HtRuleset*)h)->c.blob;
-    const uint8_t* gblob = blobv.data();
-    const RulesetHdr* hd = (const RulesetHdr*)gblob;
-    if (!(hd->flags & kFlagFastOk) || hd->off_row == 0) return -2;
-    const RowLayout L = row_layout(maxb, maxe);
-    std::vector<uint8_t> lds(L.bytes + 64, 0xA5);
-    const RowTabs T = row_tabs(gblob, blobv.data());
-    std::vector<std::vector<uint8_t>> bufs(4);
-    const uint8_t* bases[4] = {nullptr, nullptr, nullptr, nullptr};
-    V len(0u), mis(0u), r(0u);
-    M live(false);
-    for (uint32_t d = 0; d < 4; d++) {
-        bufs[d].assign((d < nd ? lens[d] : 0) + 64, 0x5A);
-        uintptr_t a = ((uintptr_t)bufs[d].data() + 15) & ~(uintptr_t)15;
-        const uint32_t m = d < nd ? (mis_in[d] & 15u) : 0u;
-        if (d < nd && lens[d]) std::memcpy((uint8_t*)a + m, docs[d], lens[d]);
-        bases[d] = (const uint8_t*)a;
-        for (int l = 0; l < 16; l++) {
-            len.x[16 * d + l] = d < nd ? lens[d] : 0u;
-            mis.x[16 * d + l] = m;
-            r.x[16 * d + l] = d;
-            if (d < nd) live.b |= 1ull << (16 * d + l);
-        }
-    }
-    auto load = [&](const V& b, const M& m) -> G16 {
-        P a;
-        for (int l = 0; l < 64; l++) a.p[l] = m.at(l) ? bases[l >> 4] + 16u * b.x[l] : nullptr;
-        return gld128(a, m);
-    };
-    M ok = row_scan(T, lds.data(), L, live, len, mis, load);
-    V hlo, hhi;
-    ok = row_finish(T, lds.data(), L, ok, mis, hlo, hhi,
-                    [&](const V&, const M&, const M&, const V&, const V&, const V&, const V&) {});
-    const uint32_t nt = hd->pad1[0] ? hd->pad1[0] : 1u;
-    ok = row_patterns(
-        gblob, lds.data(), L, ok, mis, r,
-        [&](uint32_t d, uint32_t k, uint32_t ntr, uint8_t t, int32_t e) {
-            tri[d * ntr + k] = t;
-            if (err) err[d * ntr + k] = e;
-        },
-        [&](uint32_t d, uint32_t k, uint64_t word) {
-            if (bm) bm[(size_t)d * bm_words + k] = word;
-        },
-        bm ? bm_words : 0u);
-    (void)nt;
-    int acc = 0;
-    for (uint32_t d = 0; d < nd; d++)
-        if (ok.at(16 * d)) acc |= 1 << d;
-    return acc;
-}
-
-// the row kernel for one document: -1 exact scan, -2 no row tables, else the tri-state
-// of the (first) tree; res[p] per pattern from the bitmap (and the static errors / the
-// undecided-by-design patterns as the fold sees them)
-extern "C" int rt_eval(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
-                       uint32_t maxb, uint32_t maxe) {
+// The lean scan (ajx_lean.h) for one document: -1 exact scan, -2 not eligible, else the
+// tri-state; res[p] per pattern; row_out (optional, 1 + n_selectors) the capture row.
+extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
+                                uint64_t* row_out) {
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
     const RulesetHdr* hd = (const RulesetHdr*)blob;
-    const uint32_t nt = hd->pad1[0] ? hd->pad1[0] : 1u;
-    std::vector<uint8_t> tri(nt);
-    std::vector<int32_t> errs(nt);
-    uint64_t bm[2] = {0, 0};
-    const uint8_t* docs[1] = {doc};
-    const int rc = rt_run(h, docs, &len, &mis, 1, tri.data(), errs.data(), bm, 2, maxb, maxe);
-    if (rc < 0) return rc;
-    if (!(rc & 1)) return -1;
+    if (!(hd->flags & kFlagFastOk)) return -2;
+    std::vector<uint8_t> buf(len + 96, 0x7A);  // (neighbour bytes around the document)
+    uintptr_t base = ((uintptr_t)buf.data() + 15) & ~(uintptr_t)15;
+    uint8_t* d = (uint8_t*)base + (mis & 15);
+    std::memcpy(d, doc, len);
+    std::vector<uint64_t> row(1 + hd->n_selectors, 0xDEADBEEFDEADBEEFull);
+    const uint32_t* a = (const uint32_t*)(d - (mis & 15));
+    const uint32_t nb = (uint32_t)((buf.data() + buf.size() - (const uint8_t*)a) / 16);
+    alignas(16) uint8_t ring_mem[lean::kRingStride];
+    std::memset(ring_mem, 0x5A, sizeof ring_mem);
+    auto load = [&](uint32_t b, uint32_t nblk) -> Block16 {
+        if (b < nblk && b < nb) return Block16{a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
+        return Block16{0, 0, 0, 0};
+    };
+    const bool ok = lean::scan_doc(blob, blob_tables(blob), d, len, row.data(), ring_mem, load);
+    if (!ok) return -1;
+    if (row_out) std::memcpy(row_out, row.data(), row.size() * sizeof(uint64_t));
+    uint64_t t[2], u[2];
+    patterns_from_row(blob, d, row.data(), t, u);
+    if ((u[0] & ~hd->unsupported[0]) | (u[1] & ~hd->unsupported[1])) return -1;
+    const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
     for (uint32_t p = 0; p < hd->n_patterns; p++) {
         uint64_t bit = 1ull << (p & 63);
         uint32_t k = p >> 6;
-        res[p] = (hd->static_error[k] & bit) ? V_E : (hd->unsupported[k] & bit) ? V_U : (bm[k] & bit) ? V_T : V_F;
+        res[p] = (hd->static_error[k] & bit) ? V_E : (u[k] & bit) ? V_U : (t[k] & bit) ? V_T : V_F;
     }
-    if (err) *err = errs[0];
-    return tri[0];
+    return run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
+}
+extern "C" int ht_eval_lean(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err) {
+    return ht_eval_lean_row(h, doc, len, mis, res, err, nullptr);
+}
+// the byte-class masks of 32 bytes (LUT + transpose): out[c] = mask of class c
+extern "C" void ht_lean_classes(const uint8_t* bytes, uint32_t* out) {
+    uint32_t d[8];
+    for (int j = 0; j < 8; j++) {
+        uint32_t x;
+        std::memcpy(&x, bytes + 4 * j, 4);
+        d[j] = lean::classify4(x);
+    }
+    lean::transpose(d);
+    for (uint32_t c = 0; c < 8; c++) out[c] = d[lean::creg(c)];
 }

@@ -21,8 +21,7 @@ void* ht_compile(const authjx_tree* tree, int32_t* status, char* err, size_t cap
 void ht_free(void* h);
 int ht_eval(void* h, const uint8_t* doc, uint32_t len, uint8_t* res, int32_t* err);
 int ht_eval_fast(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err);
-int rt_eval(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err, uint32_t maxb,
-            uint32_t maxe);
+int ht_eval_lean(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err);
 }
 
 static std::mt19937_64 rng;
@@ -113,7 +112,7 @@ static std::string rand_selector() {
 int main(int argc, char** argv) {
     const long iters = argc > 1 ? atol(argv[1]) : 300;
     rng.seed(argc > 2 ? (uint64_t)atoll(argv[2]) : 7);
-    long docs = 0, fast_decided = 0, row_decided = 0, bad = 0;
+    long docs = 0, fast_decided = 0, lean_decided = 0, bad = 0;
     for (long it = 0; it < iters; it++) {
         const int np = 1 + (int)rnd(8);
         std::vector<std::string> sels(np), vals(np);
@@ -147,8 +146,7 @@ int main(int argc, char** argv) {
             int32_t e0 = 0, e1 = 0, e2 = 0;
             const int t0 = ht_eval(h, (const uint8_t*)d.data(), (uint32_t)d.size(), r0.data(), &e0);
             const int t1 = ht_eval_fast(h, (const uint8_t*)d.data(), (uint32_t)d.size(), (uint32_t)rnd(16), r1.data(), &e1);
-            const int t2 = rt_eval(h, (const uint8_t*)d.data(), (uint32_t)d.size(), (uint32_t)rnd(16), r2.data(), &e2,
-                                   rnd(2) ? 8192u : 512u, rnd(2) ? 2048u : 64u);
+            const int t2 = ht_eval_lean(h, (const uint8_t*)d.data(), (uint32_t)d.size(), (uint32_t)rnd(16), r2.data(), &e2);
             docs++;
             if (t1 >= 0) {
                 fast_decided++;
@@ -158,15 +156,15 @@ int main(int argc, char** argv) {
                 }
             }
             if (t2 >= 0 && std::find(r0.begin(), r0.end(), (uint8_t)3) == r0.end()) {
-                row_decided++;
+                lean_decided++;
                 if (t2 != t0 || r2 != r0) {
-                    if (bad < 10) printf("ROW MISMATCH doc=%s\n", d.c_str());
+                    if (bad < 10) printf("LEAN MISMATCH doc=%s\n", d.c_str());
                     bad++;
                 }
             }
         }
         ht_free(h);
     }
-    printf("docs %ld fast_decided %ld row_decided %ld mismatches %ld\n", docs, fast_decided, row_decided, bad);
+    printf("docs %ld fast_decided %ld lean_decided %ld mismatches %ld\n", docs, fast_decided, lean_decided, bad);
     return bad ? 1 : 0;
 }

@@ -471,10 +471,9 @@ def test_select_from_eval_matches_select_batch(ctx):
         ctx.select_from_eval_device(fused, fused.n_patterns - k, A, Of, Ln, got)
 
 
-@pytest.mark.parametrize("mode", [0, 40])
+@pytest.mark.parametrize("mode", [0])
 def test_kernels_match_oracle(ctx, mode):
-    """The row kernel (default, ajx_row.h) and the token-scanner single-pass kernel (kernel
-    mode 40, ajx_fast.h) on the c2 / c3 workloads, random and malformed documents (and
+    """The single-pass kernel on the c2 / c3 workloads, random and malformed documents (and
     c4's multi-tenant kernel): the same outputs as the oracle."""
     import fuzz_util as FU
     from authorino_amd import workloads as W
@@ -488,7 +487,7 @@ def test_kernels_match_oracle(ctx, mode):
             assert ctx.last_exact_count() == 0  # every synthetic document stayed on the fast path
             otri, oerr, obm = _oracle(w.expr, w.arena, w.offs, w.lens)
             assert np.array_equal(tri, otri) and np.array_equal(err, oerr) and np.array_equal(bm, obm)
-        if mode == 40:
+        if True:
             w = W.make("c4", n=30000, seed=32)
             rss = [ctx.compile_expression(e) for e in w.exprs]
             tri, err, bm = ctx.eval_host_arena(rss, w.arena, w.offs, w.lens, set_of_req=w.set_of_req)
