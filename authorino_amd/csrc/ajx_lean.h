@@ -214,6 +214,12 @@ AJX_HD bool scalar_start(uint32_t b) {
            b == 'N';
 }
 
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(AJX_LEAN_COUNT)
+inline uint64_t g_lean_iters = 0, g_lean_subs = 0;  // (host test builds: walker iterations, sub-windows)
+#define AJX_LEAN_TICK(x) (x)++
+#else
+#define AJX_LEAN_TICK(x) ((void)0)
+#endif
 constexpr uint32_t kRingStride = 144;  // per lane: 4 slots of 32 B + a mirror of the first 16 B
 constexpr uint32_t kMaxLive = 16;      // containers on selector paths nested (deeper: exact scan)
 constexpr uint32_t kIdxKeyLen = kIndexKeyLen;
@@ -449,7 +455,9 @@ struct Walk {
             T = c.tok;
         }
         const uint32_t cok = (c.co >> 1) | (l.co << 31);  // bit i: a colon at byte i + 1
+        AJX_LEAN_TICK(g_lean_subs);
         while (T) {
+            AJX_LEAN_TICK(g_lean_iters);
             const uint32_t i = ctz(T);
             T &= T - 1u;
             const uint32_t p = (uint32_t)(c.base + (int32_t)i);

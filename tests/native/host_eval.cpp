@@ -9,6 +9,7 @@
 
 #include "../../authorino_amd/csrc/ajx_compiler.h"
 #include "../../authorino_amd/csrc/ajx_fast.h"
+#define AJX_LEAN_COUNT 1
 #include "../../authorino_amd/csrc/ajx_lean.h"
 #include "../../authorino_amd/csrc/ajx_modifiers.h"
 #include "../../authorino_amd/csrc/ajx_regex.h"
@@ -272,4 +273,9 @@ extern "C" void ht_lean_classes(const uint8_t* bytes, uint32_t* out) {
     }
     lean::transpose(d);
     for (uint32_t c = 0; c < 8; c++) out[c] = d[lean::creg(c)];
+}
+
+extern "C" void ht_lean_counts(uint64_t* iters, uint64_t* subs) {
+    *iters = lean::g_lean_iters;
+    *subs = lean::g_lean_subs;
 }

@@ -90,3 +90,99 @@ def test_lean_decides_workload_documents(workload):
             assert lres == tres and tl == tt and el == et
             t_or, _ = rs.matches(d)
             assert tl == t_or
+
+
+def _tree(rng, depth, keys):
+    r = rng.random()
+    if depth <= 0 or r < 0.35:
+        k = rng.integers(0, 4)
+        if k == 0:
+            return ("s", "".join(rng.choice(list("abcxyz/\\\"é -"), int(rng.integers(0, 90)))))
+        if k == 1:
+            return ("n", str(int(rng.integers(-10**9, 10**9))))
+        if k == 2:
+            return ("l", ["true", "false", "null"][rng.integers(0, 3)])
+        return ("s", "v%d" % rng.integers(0, 20))
+    n = int(rng.integers(0, 7))
+    if r < 0.75:
+        return ("o", [(keys[rng.integers(0, len(keys))], _tree(rng, depth - 1, keys)) for _ in range(n)])
+    return ("a", [_tree(rng, depth - 1, keys) for _ in range(n)])
+
+
+def _paths(v, prefix, out):
+    t, x = v
+    if t == "o":
+        for k, c in x:
+            p = prefix + [FU.esc_key(k)]
+            out.append(p)
+            _paths(c, p, out)
+    elif t == "a":
+        for i, c in enumerate(x):
+            p = prefix + [str(i)]
+            out.append(p)
+            _paths(c, p, out)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_lean_deep_trees_selectors_from_the_document(seed):
+    """Compact documents of 1-6 KiB (keys of 1..40 bytes, strings up to 90 bytes, squashed
+    containers spanning sub-windows), selectors taken from the document's own paths
+    (array indices included), every misalignment: the oracle's results, and the token
+    scanner's capture rows."""
+    rng = np.random.default_rng(300 + seed)
+    keys = ["k", "ab", "x.y", "0", "name", "a-much-longer-key-name", "key-with-sixteen", "nine-byte",
+            "a b", "the-key-name-that-goes-past-thirty-bytes", "é", "ab-tail-", "zz-tail-"]
+    decided = decided_tok = total = 0
+    for _ in range(60):
+        v = ("o", [(keys[rng.integers(0, len(keys))], _tree(rng, 5, keys)) for _ in range(int(rng.integers(2, 9)))])
+        d = FU.dump(v, rng, False).encode()
+        paths = []
+        _paths(v, [], paths)
+        if not paths:
+            continue
+        pats = []
+        for _ in range(int(rng.integers(1, 9))):
+            p = paths[int(rng.integers(0, len(paths)))]
+            pats.append((".".join(p), [1, 2, 3, 4][rng.integers(0, 4)], ["v3", "", "true", "x"][rng.integers(0, 4)]))
+        nodes, root = _chain(len(pats))
+        rs = O.Ruleset(pats, nodes, root)
+        ot = [rs.pattern(p, d) for p in range(len(pats))]
+        if O.UNSUPPORTED in ot:
+            continue
+        hr = H.HostRuleset(pats, nodes, root)
+        n_sel = len({p[0] for p in pats})
+        for mis in (0, int(rng.integers(1, 16))):
+            total += 1
+            tl, _, lres, lrow = H.eval_lean(hr, d, mis=mis, n_sel=n_sel)
+            tt, _, tres, trow = H.eval_tok(hr, d, mis=mis, n_sel=n_sel)
+            decided_tok += tt >= 0
+            if tl >= 0:
+                decided += 1
+                assert lres == ot, (pats, d)
+                if tt >= 0:
+                    assert lrow == trow, (pats, d, mis)
+    # (selectors into containers nested in indexed arrays, deep index chains: the exact
+    # scan, by design, for both scanners)
+    assert decided >= decided_tok and decided >= 0.1 * total, (decided, decided_tok, total)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_lean_long_values(seed):
+    """Selector values that are long strings / arrays after long padding (they straddle
+    sub-windows and 64-byte windows)."""
+    rng = np.random.default_rng(400 + seed)
+    n = 0
+    for _ in range(150):
+        pats = FU.rand_patterns(rng, int(rng.integers(1, 6)))
+        nodes, root = _chain(len(pats))
+        rs = O.Ruleset(pats, nodes, root)
+        d = FU.long_doc(rng, pats)
+        ot = [rs.pattern(p, d) for p in range(len(pats))]
+        if O.UNSUPPORTED in ot:
+            continue
+        hr = H.HostRuleset(pats, nodes, root)
+        tl, _, lres, _ = H.eval_lean(hr, d, mis=int(rng.integers(0, 16)))
+        if tl >= 0 and 3 not in lres:
+            n += 1
+            assert lres == ot, (pats, d)
+    assert n > 80
