@@ -120,7 +120,8 @@ constexpr uint8_t kNoNode = 0xFF;
 struct TrieNode {
     uint16_t child_begin;  // index into TrieChild[]
     uint8_t n_children;
-    uint8_t flags;         // bit0: has array-index children
+    uint8_t flags;         // bit0: has array-index children; bit1: a leaf with eager
+                           // incl/excl patterns (the lean scan walks its array value)
     int16_t selector;      // selector whose path ends here, -1 none
     uint16_t pad;
 };
@@ -208,13 +209,26 @@ struct RulesetHdr {
                                 // (selectors, components, modifiers follow: exact scan only)
     uint32_t key_probes;        // every key sits within key_probes slots of its home slot
     uint32_t key_mult;          // key_slot_hash multiplier
-    uint32_t pad2[3];
+    uint32_t off_eager;         // EagerSel[n_selectors] (0: none)
+    uint32_t pad2[2];
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
     uint64_t unsupported[2];    // pattern p can not be decided on the device
 };
 constexpr uint32_t kFlagFastOk = 4;
 
-constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the exact scan's buffers
+constexpr uint32_t kFlagBufs = 8;
+
+// Patterns the lean scan decides while it captures (ajx_lean.h): per selector, its first
+// two patterns (index < 64) that compare an unescaped string value's text with a literal
+// of at most 16 bytes (eq, neq, incl / excl on the value alone), and incl / excl over
+// an array of unescaped strings. m: pattern | op << 8 | literal length << 16 | 1 << 31.
+struct EagerSel {
+    uint32_t lit[2][4];
+    uint32_t m[2];
+    uint32_t pad[2];
+};
+static_assert(sizeof(EagerSel) == 48, "EagerSel layout");
+constexpr uint32_t kEagerValid = 1u << 31;  // a selector builds a text (a '#' list): the exact scan's buffers
 
 }  // namespace ajx

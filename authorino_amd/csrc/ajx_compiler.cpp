@@ -746,6 +746,35 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         b.append(tc.data(), tc.size() * sizeof(TrieChild));
         hdr.off_key_slots = (uint32_t)b.align16();
         b.append(slots.data(), slots.size() * sizeof(KeySlot));
+        // eager patterns (ajx_lean.h): per selector its first two eq / neq / incl / excl
+        // patterns with a literal of <= 16 bytes (pattern index < 64)
+        if (fast_ok) {
+            std::vector<EagerSel> eg(sels.size(), EagerSel{});
+            bool any = false;
+            for (size_t sidx = 0; sidx < sels.size(); sidx++) {
+                uint32_t k = 0;
+                bool arr_ops = false;
+                for (uint16_t pi : sel_pats[sidx]) {
+                    const Pattern& pt = pats[pi];
+                    if (k >= 2 || pi >= 64 || pt.state != P_OK || pt.lit_len > 16) continue;
+                    if (pt.op != OP_EQ && pt.op != OP_NEQ && pt.op != OP_INCL && pt.op != OP_EXCL) continue;
+                    if (pt.lit_len) std::memcpy(eg[sidx].lit[k], lits.data() + pt.lit_off, pt.lit_len);
+                    eg[sidx].m[k] = (uint32_t)pi | ((uint32_t)pt.op << 8) | (pt.lit_len << 16) | kEagerValid;
+                    arr_ops = arr_ops || pt.op == OP_INCL || pt.op == OP_EXCL;
+                    k++;
+                    any = true;
+                }
+                if (arr_ops)
+                    for (size_t i = 0; i < trie.size(); i++)
+                        if (trie[i].selector == (int16_t)sidx) tn[i].flags |= 2;
+            }
+            if (any) {
+                hdr.off_eager = (uint32_t)b.align16();
+                b.append(eg.data(), eg.size() * sizeof(EagerSel));
+                // (the trie nodes were appended before their eager flags were set: rewrite)
+                std::memcpy(b.blob.data() + hdr.off_trie_nodes, tn.data(), tn.size() * sizeof(TrieNode));
+            }
+        }
         std::vector<SelectorPatterns> sp(sels.size());
         std::vector<uint16_t> plist;
         for (size_t s = 0; s < sels.size(); s++) {

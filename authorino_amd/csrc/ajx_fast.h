@@ -1099,7 +1099,7 @@ AJX_HD bool incl_hits(const uint8_t* doc, const ValueRef& v, const Pattern* pats
 // Stage B for one request: patterns on the captured values, bitmap, fold.
 // res(p) values are V_T / V_F / V_E / V_U.
 AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef row, uint64_t t[2],
-                              uint64_t u[2]) {
+                              uint64_t u[2], const uint64_t* dec = nullptr) {
     // selector by selector: each captured value is decoded once for all its patterns;
     // when its String() is a byte span or a literal, eq/neq compare a dword at a time,
     // `matches` runs the DFA straight over the span and incl/excl walk a compact array
@@ -1121,6 +1121,10 @@ AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef ro
             t1 |= sps[s].mask[1] & nt1;
             continue;
         }
+        if (dec && !(sps[s].mask[0] & ~dec[0]) && !sps[s].mask[1]) {  // decided while capturing
+            t0 |= sps[s].mask[0] & dec[1];
+            continue;
+        }
         const uint64_t rec = row[1 + s];
         const uint32_t meta = (uint32_t)(rec >> 32);
         ValueRef v;
@@ -1136,7 +1140,9 @@ AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef ro
             const uint32_t p = plist[begin + j];
             const Pattern pt = pats[p];
             uint8_t r;
-            if (pt.state != P_OK) {
+            if (dec && p < 64 && ((dec[0] >> p) & 1u)) {
+                r = ((dec[1] >> p) & 1u) ? V_T : V_F;
+            } else if (pt.state != P_OK) {
                 r = pt.state == P_STATIC_E ? V_E : V_U;
             } else if (rv.ok && (pt.op == OP_EQ || pt.op == OP_NEQ)) {
                 r = raw_equals(doc, rv, pt, lits) == (pt.op == OP_EQ) ? V_T : V_F;

@@ -282,10 +282,11 @@ __device__ __forceinline__ void fold_outputs(uint32_t r, const uint8_t* blob, co
 // decides), the caller hands the request over
 __device__ __forceinline__ bool finish_request(uint32_t r, const uint8_t* blob, const uint8_t* d, RowRef row,
                                                uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-                                               uint64_t* __restrict__ out_bm, uint32_t stride) {
+                                               uint64_t* __restrict__ out_bm, uint32_t stride,
+                                               const uint64_t* dec = nullptr) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     uint64_t t[2], u[2];
-    patterns_from_row(blob, d, row, t, u);
+    patterns_from_row(blob, d, row, t, u, dec);
     if ((u[0] & ~h->unsupported[0]) | (u[1] & ~h->unsupported[1])) return false;
     if (out_bm) {
         uint64_t* orow = out_bm + (size_t)r * stride;
@@ -393,6 +394,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_lean(
     const uint32_t len = lens[r];
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     bool ok = (h->flags & kFlagFastOk) && len < (1u << 24);
+    uint64_t dec[2] = {0ull, 0ull};
     if (ok) {
         const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
         auto load = [&](uint32_t b, uint32_t nblk) -> Block16 {
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_lean(
             }
             return Block16{0u, 0u, 0u, 0u};
         };
-        ok = lean::scan_doc(blob, blob_tables(blob), d, len, row, ring, load);
+        ok = lean::scan_doc(blob, blob_tables(blob), d, len, row, ring, load, dec);
     } else {
         row[0] = kRowSlow;
     }
@@ -414,7 +416,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_lean(
     out_tri[r] = (uint8_t)row[0];
     return;
 #endif
-    if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
+    if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec)) {
         row[0] = kRowSlow;
         slow_ids[atomicAdd(slow_count, 1u)] = r;
     }

@@ -252,6 +252,11 @@ struct Walk {
     uint32_t lbs1;          // last backslash before it, + 1 (0 none)
     int32_t root_end;       // position of the root's close
     uint64_t found;
+    // eager patterns (EagerSel, ajx_blob.h): decided (eD) and true (eT) bits of patterns < 64;
+    // ea: the open eager array (selector + 1 | depth << 8 | entry hits << 16 | dirty << 18)
+    const EagerSel* eg;
+    uint64_t eT, eD;
+    uint32_t ea;
 
     AJX_HD uint32_t rb(uint32_t p) const { return ring[(p + mis) & 127u]; }  // doc byte p (ring)
     AJX_HD uint32_t r32(uint32_t a) const {  // 4 ring bytes from ring offset a (0..127)
@@ -292,6 +297,64 @@ struct Walk {
         found |= 1ull << s;
         row[1 + (uint32_t)s] =
             (uint64_t)start | ((uint64_t)(((end - start) & 0xFFFFFFu) | (type << 24) | (esc << 27)) << 32);
+        if (eg && type == T_STRING && !esc) {  // the selector's eager patterns on the value alone
+            const EagerSel e = eg[s];
+            const uint32_t mt = eager_match(e, start + 1u, end - start - 2u);
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const uint32_t m = e.m[k], op = (m >> 8) & 0xFFu;
+                const uint64_t bit = 1ull << (m & 63u);
+                const bool yes = ((mt >> k) & 1u) == (op == OP_EQ || op == OP_INCL ? 1u : 0u);
+                eD = (m & kEagerValid) ? eD | bit : eD;
+                eT = (m & kEagerValid) && yes ? eT | bit : eT;
+            }
+        }
+    }
+    // bit k: entry k's literal equals the string content [a, a + cl) (ring bytes; cl <= 16
+    // for a match, and then the content lies in the ring's window)
+    AJX_HD uint32_t eager_match(const EagerSel& e, uint32_t a, uint32_t cl) const {
+        uint64_t c0 = 0, c1 = 0;
+        if (cl <= 16) {
+            c0 = r64((a + mis) & 127u);
+            c1 = r64((a + 8u + mis) & 127u);
+        }
+        const uint64_t m0 = cl >= 8 ? ~0ull : ((1ull << (8 * cl)) - 1ull);
+        const uint64_t m1 = cl >= 16 ? ~0ull : (cl > 8 ? ((1ull << (8 * (cl - 8))) - 1ull) : 0ull);
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint64_t l0 = (uint64_t)e.lit[k][0] | ((uint64_t)e.lit[k][1] << 32);
+            const uint64_t l1 = (uint64_t)e.lit[k][2] | ((uint64_t)e.lit[k][3] << 32);
+            const bool eq = (e.m[k] & kEagerValid) && cl == ((e.m[k] >> 16) & 0xFFu) && ((c0 ^ l0) & m0) == 0 &&
+                            ((c1 ^ l1) & m1) == 0;
+            r |= eq ? 1u << k : 0u;
+        }
+        return r;
+    }
+    // an element of the open eager array: a string's content (hits), else the array is left
+    // to stage B
+    AJX_HD void eager_elem(bool str, uint32_t a, uint32_t cl, bool esc) {
+        if (!ea || (ea >> 8 & 0xFFu) != depth) return;
+        if (!str || esc) {
+            ea |= 1u << 18;
+            return;
+        }
+        ea |= eager_match(eg[(ea & 0xFFu) - 1u], a, cl) << 16;
+    }
+    AJX_HD void eager_close() {
+        if (!ea || (ea >> 8 & 0xFFu) != depth) return;
+        if (!((ea >> 18) & 1u)) {
+            const EagerSel e = eg[(ea & 0xFFu) - 1u];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const uint32_t m = e.m[k], op = (m >> 8) & 0xFFu;
+                if (!(m & kEagerValid) || (op != OP_INCL && op != OP_EXCL)) continue;
+                const uint64_t bit = 1ull << (m & 63u);
+                eD |= bit;
+                if (((ea >> (16 + k)) & 1u) == (op == OP_INCL ? 1u : 0u)) eT |= bit;
+            }
+        }
+        ea = 0;
     }
     // the key table: (sig, len, parent) -> child node (kNoNode none). len = kIdxKeyLen:
     // sig is an array index. A hit on a key longer than 8 bytes also compares its head
@@ -339,7 +402,8 @@ struct Walk {
     // a container value at p ('{' or '['), node = its trie node
     AJX_HD void open(uint32_t node, bool arr, uint32_t p) {
         const int32_t s = leaf_sel(node);
-        if (node == kNoNode || tn[node].n_children == 0) {  // squashed (captured when a leaf)
+        const bool eager = arr && eg && s >= 0 && !ea && (tn[node].flags & 2);  // (its elements compared)
+        if (node == kNoNode || (tn[node].n_children == 0 && !eager)) {  // squashed (captured when a leaf)
             skipd = 1;
             skipcap = s >= 0 ? (uint32_t)s + 1u : 0u;
             skips = p;
@@ -363,6 +427,7 @@ struct Walk {
         tarr = arr ? 1u : 0u;
         expk = 1;
         idx = 0;
+        if (eager) ea = ((uint32_t)s + 1u) | (depth << 8);
         if (s >= 0) {
             found |= 1ull << s;  // (first match in document order)
             if (ncap >= 2) { st = S_SLOW; return; }
@@ -375,6 +440,7 @@ struct Walk {
         }
     }
     AJX_HD void close(uint32_t p) {
+        eager_close();
         if (ncap) {
             const uint32_t cs = ncap == 2 ? cap1 : cap0, start = ncap == 2 ? cap1s : cap0s;
             if ((cs >> 8) == depth) {
@@ -476,9 +542,11 @@ struct Walk {
                 if (tarr) {  // a string element
                     const uint32_t node = elem_node();
                     const int32_t s = leaf_sel(node);
-                    if (s >= 0) {
+                    if (s >= 0 || ea) {
                         const uint32_t so = (c.oq & below(i)) ? (uint32_t)c.base + hib(c.oq & below(i)) : carry_oq;
-                        record(s, so, p + 1, T_STRING, has_bs(so, p, c, l) ? 1u : 0u);
+                        const bool esc = has_bs(so, p, c, l);
+                        if (s >= 0) record(s, so, p + 1, T_STRING, esc ? 1u : 0u);
+                        if (ea) eager_elem(true, so + 1u, p - so - 1u, esc);
                     }
                     continue;
                 }
@@ -538,6 +606,7 @@ struct Walk {
                     continue;
                 }
                 if (!tarr) { st = S_SLOW; T = 0; break; }  // (a container where a key belongs)
+                if (ea) eager_elem(false, 0, 0, false);
                 open(elem_node(), rb(p) == '[', p);
                 if (skipd) T &= c.op | c.cl;
                 continue;
@@ -548,6 +617,7 @@ struct Walk {
                 if (st != S_RUN) { T = 0; break; }
                 continue;
             }
+            if (ea) eager_elem(false, 0, 0, false);
             // an array element's scalar
             if (depth == 0 || !tarr) { st = S_SLOW; T = 0; break; }
             const uint32_t node = elem_node();
@@ -560,10 +630,11 @@ struct Walk {
 
 // Stage A for one request with the lean scan. `ring` = the work-item's 144-byte ring,
 // `load(b, nblk)` returns aligned 16-byte block b of the document (zeros past nblk). Returns
-// true when the capture row is valid (false: the exact scan decides the request).
+// true when the capture row is valid (false: the exact scan decides the request); dec[0] /
+// dec[1]: the patterns decided while capturing / those of them that are true.
 template <class LoadBlock>
 AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, uint32_t n, RowRef row, uint8_t* ring,
-                     LoadBlock load) {
+                     LoadBlock load, uint64_t dec[2]) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
     Walk w;
     w.tn = tab.tn;
@@ -594,6 +665,9 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     w.lbs1 = 0;
     w.root_end = 0x7FFFFFFF;
     w.found = 0;
+    w.eg = h->off_eager ? reinterpret_cast<const EagerSel*>(blob + h->off_eager) : nullptr;
+    w.eT = w.eD = 0;
+    w.ea = 0;
     Carry cr;
     cr.f = 0;
     cr.bad = 0x7FFFFFFF;
@@ -658,6 +732,8 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
         return false;
     }
     row[0] = w.found;
+    dec[0] = w.eD;
+    dec[1] = w.eT;
     return true;
 }
 

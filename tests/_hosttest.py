@@ -203,3 +203,11 @@ def lean_classes(b32: bytes):
     out = (C.c_uint32 * 8)()
     L.ht_lean_classes(bytes(b32), out)
     return list(out)
+
+
+def lean_last_dec():
+    """(decided, true) pattern bits of the last eval_lean (eager patterns)."""
+    L = _lean_decl()
+    out = (C.c_uint64 * 2)()
+    L.ht_lean_last_dec(out)
+    return out[0], out[1]

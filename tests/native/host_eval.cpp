@@ -228,6 +228,11 @@ extern "C" uint32_t ht_blob_size(void* h) { return (uint32_t)((HtRuleset*)h)->c.
 // ---------------------------------------------------------------------------------
 // The lean scan (ajx_lean.h) for one document: -1 exact scan, -2 not eligible, else the
 // tri-state; res[p] per pattern; row_out (optional, 1 + n_selectors) the capture row.
+static uint64_t g_last_dec[2];
+extern "C" void ht_lean_last_dec(uint64_t* out) {
+    out[0] = g_last_dec[0];
+    out[1] = g_last_dec[1];
+}
 extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
                                 uint64_t* row_out) {
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
@@ -246,11 +251,14 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
         if (b < nblk && b < nb) return Block16{a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
         return Block16{0, 0, 0, 0};
     };
-    const bool ok = lean::scan_doc(blob, blob_tables(blob), d, len, row.data(), ring_mem, load);
+    uint64_t dec[2] = {0, 0};
+    const bool ok = lean::scan_doc(blob, blob_tables(blob), d, len, row.data(), ring_mem, load, dec);
+    g_last_dec[0] = dec[0];
+    g_last_dec[1] = dec[1];
     if (!ok) return -1;
     if (row_out) std::memcpy(row_out, row.data(), row.size() * sizeof(uint64_t));
     uint64_t t[2], u[2];
-    patterns_from_row(blob, d, row.data(), t, u);
+    patterns_from_row(blob, d, row.data(), t, u, dec);
     if ((u[0] & ~hd->unsupported[0]) | (u[1] & ~hd->unsupported[1])) return -1;
     const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
     for (uint32_t p = 0; p < hd->n_patterns; p++) {

@@ -2,6 +2,8 @@
 build: the byte-class LUT + transpose against plain compares, and the scan + stage B
 against the oracle (and its capture rows against the token scanner's) on the workloads'
 documents, random documents, mutated bytes and selector sets with indices / duplicates."""
+import json
+
 import numpy as np
 import pytest
 
@@ -186,3 +188,57 @@ def test_lean_long_values(seed):
             n += 1
             assert lres == ot, (pats, d)
     assert n > 80
+
+
+def test_eager_patterns_decided_in_the_scan():
+    """c2's eq / neq / incl patterns with literals of <= 16 bytes are decided while the scan
+    captures (EagerSel): everything but the 35-byte iss literal; same results."""
+    from authorino_amd import workloads as W
+
+    w = W.make("c2", n=100, seed=23)
+    hr = H.HostRuleset.from_expression(w.expr)
+    rs = O.Ruleset.from_expression(w.expr)
+    for i in range(w.n):
+        d = w.doc(i)
+        t, _, res, _ = H.eval_lean(hr, d, mis=i % 16)
+        assert t >= 0 and res == [rs.pattern(p, d) for p in range(16)]
+        dm, tm = H.lean_last_dec()
+        assert bin(dm).count("1") >= 12, hex(dm)  # (iss: stage B; literals, missing keys: Null)
+        assert not (dm >> 4) & 1  # the iss pattern
+        for p in range(16):
+            if (dm >> p) & 1:
+                assert ((tm >> p) & 1) == (res[p] == 1)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_eager_arrays_and_strings(seed):
+    """incl / excl over arrays of strings (escaped elements, numbers, nested containers,
+    empty arrays, more than two patterns per selector), eq / neq on strings of 0..20 bytes."""
+    rng = np.random.default_rng(500 + seed)
+    words = ["", "a", "users", "reader", "admins", "x" * 16, "y" * 17, "é", "a\"b", "v3"]
+    for _ in range(200):
+        def elem():
+            r = rng.random()
+            if r < 0.7:
+                return json.dumps(words[rng.integers(0, len(words))])
+            if r < 0.8:
+                return "12"
+            if r < 0.9:
+                return "[\"users\"]"
+            return "true"
+        arrs = {k: "[" + ",".join(elem() for _ in range(int(rng.integers(0, 5)))) + "]" for k in ("g", "r")}
+        strs = {k: json.dumps(words[rng.integers(0, len(words))]) for k in ("s", "t")}
+        vals = {**arrs, **strs}
+        d = ("{" + ",".join('"%s":%s' % (k, v) for k, v in vals.items()) + "}").encode()
+        pats = []
+        for _ in range(int(rng.integers(1, 7))):
+            sel = ["g", "r", "s", "t"][rng.integers(0, 4)]
+            op = [1, 2, 3, 4][rng.integers(0, 4)]
+            pats.append((sel, op, words[rng.integers(0, len(words))]))
+        nodes, root = _chain(len(pats))
+        rs = O.Ruleset(pats, nodes, root)
+        hr = H.HostRuleset(pats, nodes, root)
+        ot = [rs.pattern(p, d) for p in range(len(pats))]
+        t, _, res, _ = H.eval_lean(hr, d, mis=int(rng.integers(0, 16)))
+        if t >= 0 and 3 not in res:
+            assert res == ot, (pats, d)
