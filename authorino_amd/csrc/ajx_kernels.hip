@@ -373,6 +373,16 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
     }
 }
 
+// stage B of the lean kernel as a call (not inlined): the scan's live state ends before it,
+// so the two stages do not share one register allocation
+__device__ __attribute__((noinline)) bool lean_finish(uint32_t r, const uint8_t* blob, const uint8_t* d, RowRef row,
+                                                      uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                                      uint64_t* __restrict__ out_bm, uint32_t stride, uint64_t dec0,
+                                                      uint64_t dec1) {
+    const uint64_t dec[2] = {dec0, dec1};
+    return finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec);
+}
+
 // The lean single-pass kernel (ajx_lean.h): stage A with the lean scan, then stage B in the
 // same work-item. Dynamic LDS: [blob copy (SHARED)] [per wave: 64 lanes x 144-B rings].
 constexpr uint32_t kLeanRingBytesPerWave = 64 * lean::kRingStride;
@@ -404,7 +414,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_lean(
             }
             return Block16{0u, 0u, 0u, 0u};
         };
-        ok = lean::scan_doc(blob, blob_tables(blob), d, len, row, ring, load, dec);
+        ok = lean::scan_doc(blob, blob_tables(blob), d, len, row, ring, threadIdx.x & 63u, load, dec);
     } else {
         row[0] = kRowSlow;
     }
@@ -416,7 +426,11 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_lean(
     out_tri[r] = (uint8_t)row[0];
     return;
 #endif
+#ifdef AJX_LEAN_CALL_B  // (profiling: stage B as a call; measured slower: c2 1.54 vs 1.52 ms, c5 16.2 vs 14.6)
+    if (!lean_finish(r, blob, d, row, out_tri, out_err, out_bm, stride, dec[0], dec[1])) {
+#else
     if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec)) {
+#endif
         row[0] = kRowSlow;
         slow_ids[atomicAdd(slow_count, 1u)] = r;
     }

@@ -208,6 +208,21 @@ AJX_HD void classify(Sub& o, const uint32_t x[8], int32_t base, uint32_t valid, 
     o.tok = CQ | OP | CL | (SCS & ~nCO);
 }
 
+// values every lane of the wave holds (the lean kernel runs one ruleset per batch): in
+// scalar registers
+AJX_HD uint32_t uni(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+#else
+    return x;
+#endif
+}
+template <class P>
+AJX_HD P* unip(P* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    return (P*)(uintptr_t)((uint64_t)uni((uint32_t)v) | ((uint64_t)uni((uint32_t)(v >> 32)) << 32));
+}
+
 // gjson's value-start bytes (parseObject / parseArray): " { [ n t f + - 0-9 i I N
 AJX_HD bool scalar_start(uint32_t b) {
     return b == 't' || b == 'f' || b == 'n' || b == '-' || b == '+' || (b - '0') < 10u || b == 'i' || b == 'I' ||
@@ -220,7 +235,9 @@ inline uint64_t g_lean_iters = 0, g_lean_subs = 0;  // (host test builds: walker
 #else
 #define AJX_LEAN_TICK(x) ((void)0)
 #endif
-constexpr uint32_t kRingStride = 144;  // per lane: 4 slots of 32 B + a mirror of the first 16 B
+// per lane: 4 slots of 32 B. 16-byte chunk k of a lane's ring sits at chunk k ^ (lane & 7)
+// (ring_off), so that the 8 lanes of a ds_write_b128 lane group hit all 32 banks
+constexpr uint32_t kRingStride = 128;
 constexpr uint32_t kMaxLive = 16;      // containers on selector paths nested (deeper: exact scan)
 constexpr uint32_t kIdxKeyLen = kIndexKeyLen;
 
@@ -236,7 +253,8 @@ struct Walk {
     // document
     const uint8_t* d;  // (global: bytes the ring no longer holds)
     uint32_t n, mis;
-    const uint8_t* ring;  // the lane's 144-byte ring (LDS on the device)
+    const uint8_t* ring;  // the lane's 128-byte ring (LDS on the device)
+    uint32_t sw16;        // its chunk swizzle: (lane & 7) << 4
     RowRef row;
     // walker state
     uint32_t st, depth;
@@ -258,11 +276,12 @@ struct Walk {
     uint64_t eT, eD;
     uint32_t ea;
 
-    AJX_HD uint32_t rb(uint32_t p) const { return ring[(p + mis) & 127u]; }  // doc byte p (ring)
+    AJX_HD uint32_t ro(uint32_t a) const { return ((a & 0x70u) ^ sw16) | (a & 15u); }  // ring offset a (0..127)
+    AJX_HD uint32_t rw(uint32_t q) const { return *reinterpret_cast<const uint32_t*>(ring + ro(q & 127u)); }
+    AJX_HD uint32_t rb(uint32_t p) const { return ring[ro((p + mis) & 127u)]; }  // doc byte p (ring)
     AJX_HD uint32_t r32(uint32_t a) const {  // 4 ring bytes from ring offset a (0..127)
         const uint32_t q = a & ~3u, sh = a & 3u;
-        const uint32_t w0 = *reinterpret_cast<const uint32_t*>(ring + q);
-        const uint32_t w1 = *reinterpret_cast<const uint32_t*>(ring + q + 4);
+        const uint32_t w0 = rw(q), w1 = rw(q + 4);
 #if defined(__HIP_DEVICE_COMPILE__)
         return __builtin_amdgcn_alignbyte(w1, w0, sh);
 #else
@@ -271,9 +290,7 @@ struct Walk {
     }
     AJX_HD uint64_t r64(uint32_t a) const {
         const uint32_t q = a & ~3u, sh = a & 3u;
-        const uint32_t w0 = *reinterpret_cast<const uint32_t*>(ring + q);
-        const uint32_t w1 = *reinterpret_cast<const uint32_t*>(ring + q + 4);
-        const uint32_t w2 = *reinterpret_cast<const uint32_t*>(ring + q + 8);
+        const uint32_t w0 = rw(q), w1 = rw(q + 4), w2 = rw(q + 8);
 #if defined(__HIP_DEVICE_COMPILE__)
         const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
 #else
@@ -628,26 +645,28 @@ struct Walk {
     }
 };
 
-// Stage A for one request with the lean scan. `ring` = the work-item's 144-byte ring,
+// Stage A for one request with the lean scan. `ring` = the work-item's 128-byte ring (lane:
+// its lane in the wave, for the chunk swizzle),
 // `load(b, nblk)` returns aligned 16-byte block b of the document (zeros past nblk). Returns
 // true when the capture row is valid (false: the exact scan decides the request); dec[0] /
 // dec[1]: the patterns decided while capturing / those of them that are true.
 template <class LoadBlock>
 AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, uint32_t n, RowRef row, uint8_t* ring,
-                     LoadBlock load, uint64_t dec[2]) {
+                     uint32_t lane, LoadBlock load, uint64_t dec[2]) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
     Walk w;
-    w.tn = tab.tn;
-    w.ks = tab.ks;
-    w.lits = blob + h->off_literals;
-    w.ks_mask = (1u << h->key_slots_log2) - 1u;
-    w.ks_probes = h->key_probes;
-    w.ks_mult = h->key_mult;
-    w.ks_shift = 32u - h->key_slots_log2;
+    w.tn = unip(tab.tn);
+    w.ks = unip(tab.ks);
+    w.lits = unip(blob + h->off_literals);
+    w.ks_mask = uni((1u << h->key_slots_log2) - 1u);
+    w.ks_probes = uni(h->key_probes);
+    w.ks_mult = uni(h->key_mult);
+    w.ks_shift = uni(32u - h->key_slots_log2);
     w.d = d;
     w.n = n;
     w.mis = (uint32_t)((uintptr_t)d & 15u);
     w.ring = ring;
+    w.sw16 = (lane & 7u) << 4;
     w.row = row;
     w.st = S_RUN;
     w.depth = 0;
@@ -665,7 +684,7 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     w.lbs1 = 0;
     w.root_end = 0x7FFFFFFF;
     w.found = 0;
-    w.eg = h->off_eager ? reinterpret_cast<const EagerSel*>(blob + h->off_eager) : nullptr;
+    w.eg = uni(h->off_eager) ? unip(reinterpret_cast<const EagerSel*>(blob + uni(h->off_eager))) : nullptr;
     w.eT = w.eD = 0;
     w.ea = 0;
     Carry cr;
@@ -685,35 +704,35 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     auto put = [&](uint32_t slot0, const Block16* b) {  // a 64-byte window into ring slots slot0, slot0 + 1
 #pragma unroll
         for (int q = 0; q < 4; q++)
-            *reinterpret_cast<Block16*>(ring + slot0 * 32u + 16u * (uint32_t)q) = b[q];
-        if (slot0 == 0) *reinterpret_cast<Block16*>(ring + 128) = b[0];
+            *reinterpret_cast<Block16*>(ring + w.ro(slot0 * 32u + 16u * (uint32_t)q)) = b[q];
     };
-    Block16 cur[4], nxt[4];
+    // registers hold only the window on its way in (issued one sub-window's walk ahead of
+    // its use); the halves classified later are read back from the ring
+    Block16 nxt[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) cur[j] = load((uint32_t)j, nblk);
-#pragma unroll
-    for (int j = 0; j < 4; j++) nxt[j] = load(4u + (uint32_t)j, nblk);
-    put(0, cur);
+    for (int j = 0; j < 4; j++) nxt[j] = load((uint32_t)j, nblk);
+    put(0, nxt);
     Sub s0, s1, s2;
     {
-        const uint32_t x0[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+        const uint32_t x0[8] = {nxt[0].x, nxt[0].y, nxt[0].z, nxt[0].w, nxt[1].x, nxt[1].y, nxt[1].z, nxt[1].w};
         classify(s0, x0, -(int32_t)mis, valid_of(-(int32_t)mis), cr);
-        const uint32_t x1[8] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w};
+        const uint32_t x1[8] = {nxt[2].x, nxt[2].y, nxt[2].z, nxt[2].w, nxt[3].x, nxt[3].y, nxt[3].z, nxt[3].w};
         classify(s1, x1, 32 - (int32_t)mis, valid_of(32 - (int32_t)mis), cr);
     }
     for (uint32_t win = 0; win < nwin; win++) {
         const int32_t b0 = (int32_t)(win * 64u) - (int32_t)mis;
+        const bool more = win + 1 < nwin;
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) nxt[j] = load((win + 1) * 4u + (uint32_t)j, nblk);
+        }
         w.walk(s0, s1);
         if (w.st != S_RUN) break;
-        // the next window into the ring (slots of the sub-windows before this one), the
-        // one after it on its way
-        if (win + 1 < nwin) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) cur[j] = nxt[j];
-#pragma unroll
-            for (int j = 0; j < 4; j++) nxt[j] = load((win + 2) * 4u + (uint32_t)j, nblk);
-            put(((win + 1) & 1u) * 2u, cur);
-            const uint32_t x2[8] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+        // the next window into the ring (the slots of the sub-windows before this one)
+        const uint32_t slot = ((win + 1) & 1u) * 2u;
+        if (more) {
+            put(slot, nxt);
+            const uint32_t x2[8] = {nxt[0].x, nxt[0].y, nxt[0].z, nxt[0].w, nxt[1].x, nxt[1].y, nxt[1].z, nxt[1].w};
             classify(s2, x2, b0 + 64, valid_of(b0 + 64), cr);
         } else {
             s2.base = b0 + 64;
@@ -721,8 +740,10 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
         }
         w.walk(s1, s2);
         if (w.st != S_RUN) break;
-        if (win + 1 < nwin) {
-            const uint32_t x3[8] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w, cur[3].x, cur[3].y, cur[3].z, cur[3].w};
+        if (more) {
+            const Block16 h0 = *reinterpret_cast<const Block16*>(ring + w.ro(slot * 32u + 32u));
+            const Block16 h1 = *reinterpret_cast<const Block16*>(ring + w.ro(slot * 32u + 48u));
+            const uint32_t x3[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
             classify(s1, x3, b0 + 96, valid_of(b0 + 96), cr);
         }
         s0 = s2;

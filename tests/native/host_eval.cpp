@@ -252,7 +252,7 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
         return Block16{0, 0, 0, 0};
     };
     uint64_t dec[2] = {0, 0};
-    const bool ok = lean::scan_doc(blob, blob_tables(blob), d, len, row.data(), ring_mem, load, dec);
+    const bool ok = lean::scan_doc(blob, blob_tables(blob), d, len, row.data(), ring_mem, (uint32_t)mis * 5u, load, dec);
     g_last_dec[0] = dec[0];
     g_last_dec[1] = dec[1];
     if (!ok) return -1;
