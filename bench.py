@@ -391,7 +391,12 @@ def main():
         with open(args.pmc_json) as f:
             pmc = json.load(f).get(args.workload, {})
         # (measured by scripts/pmc_traffic.py on the same workload, size and kernel)
-        if pmc.get("n") == w.n and args.kernel_mode in (0, 20) and (args.kernel_mode == 20) == ("lane" in pmc.get("kernel", "")):
+        # (the kernel the counters were taken on: the lean kernel for one ruleset, the
+        # tenant kernel for a multi-tenant batch, the token scanner on kernel mode 40)
+        kname = ("ajx_scan_fused_tenant" if w.set_of_req is not None else
+                 "ajx_scan_fused" if args.kernel_mode == 40 else "ajx_scan_lean")
+        if pmc.get("n") == w.n and args.kernel_mode in (0, 40) and kname in pmc.get("kernel", "") and \
+                (kname != "ajx_scan_fused" or "tenant" not in pmc.get("kernel", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_note = pmc.get("note")
     except (OSError, ValueError):
