@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -38,10 +39,17 @@ struct Workspace {
     uint64_t id = 0;  // registry id (ruleset users)
     std::mutex mu;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // ev1: end of the last batch on this stream
-    const uint8_t** d_sets = nullptr;
-    uint32_t sets_cap = 0;
+    // the ruleset pointer table the kernels index by set_of_req: two slots (device + pinned
+    // source each), so a batch over another ruleset list fills the slot the batch before
+    // the last one used (its event, not a stream synchronize, guards the reuse)
+    const uint8_t** d_sets = nullptr;  // the current slot's device table
+    const uint8_t** d_sets_base = nullptr;
+    const uint8_t** h_sets_base = nullptr;
+    uint32_t sets_cap = 0;  // entries per slot
+    uint32_t sets_slot = 0;
+    hipEvent_t sets_ev[2] = {nullptr, nullptr};
+    bool sets_ev_rec[2] = {false, false};
     std::vector<const uint8_t*> last_sets;
-    const uint8_t** h_sets_pinned = nullptr;
     uint32_t* d_slow = nullptr;  // [0] = count, [1..] = ids: requests for the exact scan
     uint32_t slow_cap = 0;
     uint64_t* d_rows = nullptr;  // stage-A capture rows
@@ -123,8 +131,10 @@ void destroy_workspace(Workspace* w) {
                 break;
             }
     }
-    if (w->d_sets) (void)hipFree(w->d_sets);
-    if (w->h_sets_pinned) (void)hipHostFree(w->h_sets_pinned);
+    if (w->d_sets_base) (void)hipFree(w->d_sets_base);
+    if (w->h_sets_base) (void)hipHostFree(w->h_sets_base);
+    for (int k = 0; k < 2; k++)
+        if (w->sets_ev[k]) (void)hipEventDestroy(w->sets_ev[k]);
     if (w->d_slow) (void)hipFree(w->d_slow);
     if (w->d_rows) (void)hipFree(w->d_rows);
     if (w->d_perm) (void)hipFree(w->d_perm);
@@ -140,21 +150,31 @@ int ensure_sets(Workspace* w, int device, const authjx_ruleset* const* sets, uin
         ptrs[i] = sets[i]->d_blob;
     }
     if (ptrs == w->last_sets) return AUTHJX_OK;
-    // the table and its pinned source may still be read by this stream's previous batch
-    HIP_OK(hipStreamSynchronize(w->stream));
-    if (n_sets > w->sets_cap) {
-        if (w->d_sets) (void)hipFree(w->d_sets);
-        if (w->h_sets_pinned) (void)hipHostFree(w->h_sets_pinned);
+    if (n_sets > w->sets_cap) {  // (grows: the stream's previous batches may read the old table)
+        HIP_OK(hipStreamSynchronize(w->stream));
+        if (w->d_sets_base) (void)hipFree(w->d_sets_base);
+        if (w->h_sets_base) (void)hipHostFree(w->h_sets_base);
+        w->d_sets_base = nullptr;
+        w->h_sets_base = nullptr;
         w->d_sets = nullptr;
-        w->h_sets_pinned = nullptr;
         w->sets_cap = 0;
+        w->sets_ev_rec[0] = w->sets_ev_rec[1] = false;
         uint32_t cap = n_sets < 64 ? 64 : n_sets;
-        HIP_OK(hipMalloc(&w->d_sets, cap * sizeof(uint8_t*)));
-        HIP_OK(hipHostMalloc(&w->h_sets_pinned, cap * sizeof(uint8_t*), hipHostMallocDefault));
+        HIP_OK(hipMalloc(&w->d_sets_base, 2 * cap * sizeof(uint8_t*)));
+        HIP_OK(hipHostMalloc(&w->h_sets_base, 2 * cap * sizeof(uint8_t*), hipHostMallocDefault));
+        for (int k = 0; k < 2; k++)
+            if (!w->sets_ev[k]) HIP_OK(hipEventCreateWithFlags(&w->sets_ev[k], hipEventDisableTiming));
         w->sets_cap = cap;
     }
-    std::memcpy(w->h_sets_pinned, ptrs.data(), n_sets * sizeof(uint8_t*));
-    HIP_OK(hipMemcpyAsync(w->d_sets, w->h_sets_pinned, n_sets * sizeof(uint8_t*), hipMemcpyHostToDevice, w->stream));
+    // the other slot: free once the last batch that used it has finished
+    const uint32_t k = w->d_sets ? 1u - w->sets_slot : 0u;
+    if (w->sets_ev_rec[k]) HIP_OK(hipEventSynchronize(w->sets_ev[k]));
+    const uint8_t** h = w->h_sets_base + (size_t)k * w->sets_cap;
+    const uint8_t** dv = w->d_sets_base + (size_t)k * w->sets_cap;
+    std::memcpy(h, ptrs.data(), n_sets * sizeof(uint8_t*));
+    HIP_OK(hipMemcpyAsync(dv, h, n_sets * sizeof(uint8_t*), hipMemcpyHostToDevice, w->stream));
+    w->sets_slot = k;
+    w->d_sets = dv;
     w->last_sets = ptrs;
     return AUTHJX_OK;
 }
@@ -209,6 +229,10 @@ struct WsLock {
 // this workspace as a user
 int batch_done(Workspace* w, const authjx_ruleset* const* sets, uint32_t n_sets) {
     HIP_OK(hipEventRecord(w->ev1, w->stream));
+    if (w->sets_ev[w->sets_slot]) {  // (the end of the last batch that read this set-table slot)
+        HIP_OK(hipEventRecord(w->sets_ev[w->sets_slot], w->stream));
+        w->sets_ev_rec[w->sets_slot] = true;
+    }
     w->ran = true;
     for (uint32_t i = 0; i < n_sets; i++) const_cast<authjx_ruleset*>(sets[i])->note_use(w->id);
     return AUTHJX_OK;
@@ -648,17 +672,28 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
 
 }  // extern "C"
 
+constexpr uint32_t kBatcherWorkers = 2;  // one packs and launches while the other's batch runs
+
 struct authjx_batcher {
     authjx_ctx* ctx = nullptr;
-    hipStream_t stream = nullptr;  // its own stream: its own workspace in ctx
-    uint8_t* h_buf = nullptr;      // pinned staging: arena | offs | lens | set_of_req | outputs
-    size_t h_cap = 0;
-    uint8_t* d_buf = nullptr;
-    size_t d_cap = 0;
+    // per worker: its own stream (its own workspace in ctx) and staging buffers
+    struct Lane {
+        hipStream_t stream = nullptr;
+        uint8_t* h_buf = nullptr;  // pinned staging: arena | offs | lens | set_of_req | outputs
+        size_t h_cap = 0;
+        uint8_t* d_buf = nullptr;
+        size_t d_cap = 0;
+    } lanes[kBatcherWorkers];
     ajx::BatchCore* core = nullptr;
 
-    // one batch (ordered by ruleset): pack, one launch, outputs back (worker thread only)
-    int evaluate(std::vector<ajx::BatchReq*>& reqs) {
+    // one batch (ordered by ruleset): pack, one launch, outputs back (worker `wid` only)
+    int evaluate(std::vector<ajx::BatchReq*>& reqs, uint32_t wid) {
+        Lane& L = lanes[wid];
+        hipStream_t stream = L.stream;
+        uint8_t*& h_buf = L.h_buf;
+        size_t& h_cap = L.h_cap;
+        uint8_t*& d_buf = L.d_buf;
+        size_t& d_cap = L.d_cap;
         const uint32_t n = (uint32_t)reqs.size(), nt = reqs[0]->n_out;
         std::vector<const authjx_ruleset*> sets;
         std::vector<uint32_t> sor(n);
@@ -730,35 +765,41 @@ int authjx_batcher_create(authjx_ctx* ctx, uint32_t max_batch, uint32_t window_u
     HIP_OK(hipSetDevice(ctx->device));
     authjx_batcher* b = new authjx_batcher();
     b->ctx = ctx;
-    if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete b;
-        return AUTHJX_EDEVICE;
-    }
-    b->core = new ajx::BatchCore(max_batch, (uint64_t)window_us * 1000ull, queue_cap ? queue_cap : 4 * max_batch,
-                                 [b](std::vector<ajx::BatchReq*>& reqs) { return b->evaluate(reqs); });
+    for (auto& L : b->lanes)
+        if (hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) != hipSuccess) {
+            for (auto& M : b->lanes)
+                if (M.stream) (void)hipStreamDestroy(M.stream);
+            delete b;
+            return AUTHJX_EDEVICE;
+        }
+    b->core = new ajx::BatchCore(
+        max_batch, (uint64_t)window_us * 1000ull, queue_cap ? queue_cap : 4 * max_batch,
+        [b](std::vector<ajx::BatchReq*>& reqs, uint32_t wid) { return b->evaluate(reqs, wid); }, kBatcherWorkers);
     *out = b;
     return AUTHJX_OK;
 }
 
 void authjx_batcher_destroy(authjx_batcher* b) {
     if (!b) return;
-    delete b->core;  // evaluates what is queued, joins the worker
+    delete b->core;  // evaluates what is queued, joins the workers
     (void)hipSetDevice(b->ctx->device);
-    if (b->stream) (void)hipStreamSynchronize(b->stream);
-    if (b->h_buf) (void)hipHostFree(b->h_buf);
-    if (b->d_buf) (void)hipFree(b->d_buf);
-    {
-        // the context keeps the stream's workspace until shutdown; the stream goes now
-        std::lock_guard<std::mutex> g(b->ctx->mu);
-        for (size_t i = 0; i < b->ctx->ws.size(); i++)
-            if (b->ctx->ws[i]->stream == b->stream) {
-                if (b->ctx->last_ws == b->ctx->ws[i]) b->ctx->last_ws = nullptr;
-                destroy_workspace(b->ctx->ws[i]);
-                b->ctx->ws.erase(b->ctx->ws.begin() + (long)i);
-                break;
-            }
+    for (auto& L : b->lanes) {
+        if (L.stream) (void)hipStreamSynchronize(L.stream);
+        if (L.h_buf) (void)hipHostFree(L.h_buf);
+        if (L.d_buf) (void)hipFree(L.d_buf);
+        {
+            // the context keeps the stream's workspace until shutdown; the stream goes now
+            std::lock_guard<std::mutex> g(b->ctx->mu);
+            for (size_t i = 0; i < b->ctx->ws.size(); i++)
+                if (b->ctx->ws[i]->stream == L.stream) {
+                    if (b->ctx->last_ws == b->ctx->ws[i]) b->ctx->last_ws = nullptr;
+                    destroy_workspace(b->ctx->ws[i]);
+                    b->ctx->ws.erase(b->ctx->ws.begin() + (long)i);
+                    break;
+                }
+        }
+        if (L.stream) (void)hipStreamDestroy(L.stream);
     }
-    if (b->stream) (void)hipStreamDestroy(b->stream);
     delete b;
 }
 
@@ -775,6 +816,43 @@ int authjx_batcher_eval(authjx_batcher* b, const authjx_ruleset* rs, const uint8
     r.out_tri = out_tristate;
     r.out_err = out_err_idx;
     return b->core->submit(r);
+}
+
+// Profiling only (not in authjx.h): the serving path under load. `threads` producer threads
+// each submit their share of the n requests (request i: sets[sor[i]] on arena[offs[i] ..
+// offs[i] + lens[i]); thread t takes i = t, t + threads, ...) one at a time through the
+// batcher (authjx_batcher_eval, blocking, as a serving goroutine would); lat_ns[i] = that
+// call's latency, out_tri[i] its first result; *wall_ns = the whole run.
+int authjx_debug_loadgen(authjx_batcher* b, const authjx_ruleset* const* sets, const uint32_t* sor,
+                         const uint8_t* arena, const uint64_t* offs, const uint32_t* lens, uint32_t n,
+                         uint32_t threads, uint64_t* lat_ns, uint8_t* out_tri, uint64_t* wall_ns) {
+    if (!b || !sets || !sor || !arena || !offs || !lens || !lat_ns || !out_tri || !wall_ns || threads == 0)
+        return AUTHJX_EINVAL;
+    std::atomic<int> first_rc{AUTHJX_OK};
+    const uint64_t t0 = ajx::mono_ns();
+    std::vector<std::thread> ts;
+    for (uint32_t t = 0; t < threads; t++)
+        ts.emplace_back([&, t] {
+            uint8_t tri[64];
+            for (uint32_t i = t; i < n; i += threads) {
+                const authjx_ruleset* rs = sets[sor[i]];
+                if (rs->c.n_trees > 64) {
+                    first_rc.store(AUTHJX_EINVAL);
+                    return;
+                }
+                const uint64_t a = ajx::mono_ns();
+                const int rc = authjx_batcher_eval(b, rs, arena + offs[i], lens[i], 0, tri, nullptr);
+                lat_ns[i] = ajx::mono_ns() - a;
+                out_tri[i] = tri[0];
+                if (rc != AUTHJX_OK) {
+                    int ok = AUTHJX_OK;
+                    first_rc.compare_exchange_strong(ok, rc);
+                }
+            }
+        });
+    for (auto& th : ts) th.join();
+    *wall_ns = ajx::mono_ns() - t0;
+    return first_rc.load();
 }
 
 int authjx_batcher_stats(authjx_batcher* b, uint64_t* batches, uint64_t* requests, uint64_t* expired,

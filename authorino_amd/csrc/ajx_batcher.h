@@ -4,8 +4,9 @@
 // In the reference every request's goroutine evaluates its AuthConfig's expressions
 // itself (pkg/service/auth_pipeline.go:150-164, one goroutine per evaluator; up to 10k
 // concurrent gRPC streams, main.go:69,451). Here callers submit one request each and
-// block; one worker thread
-//   - waits until max_batch requests are queued or the oldest has waited `window`,
+// block; `workers` worker threads (2 by default: one packs and launches the next batch
+// while the other's batch runs on the device) each
+//   - wait until max_batch requests are queued or the oldest has waited `window`,
 //   - takes up to max_batch of them that share the oldest one's result shape (n_trees),
 //   - completes the ones whose deadline has passed with AUTHJX_ETIMEDOUT unevaluated,
 //   - orders the rest by ruleset (AuthConfig buckets: index.bucket_order — workgroups of
@@ -66,15 +67,16 @@ struct BatchStats {
 
 class BatchCore {
    public:
-    // queue_cap 0: 4 * max_batch. evaluate(batch): fills out_tri / out_err of every
-    // request and returns an AUTHJX code (applied to the whole batch on failure)
-    using Evaluator = std::function<int(std::vector<BatchReq*>&)>;
+    // queue_cap 0: 4 * max_batch. evaluate(batch, worker): fills out_tri / out_err of every
+    // request and returns an AUTHJX code (applied to the whole batch on failure); worker is
+    // the calling worker's index (its own buffers and stream)
+    using Evaluator = std::function<int(std::vector<BatchReq*>&, uint32_t)>;
 
-    BatchCore(uint32_t max_batch, uint64_t window_ns, uint32_t queue_cap, Evaluator ev)
+    BatchCore(uint32_t max_batch, uint64_t window_ns, uint32_t queue_cap, Evaluator ev, uint32_t workers = 1)
         : max_batch_(max_batch ? max_batch : 1), window_ns_(window_ns),
           queue_cap_(queue_cap ? queue_cap : 4 * (max_batch ? max_batch : 1)),
           eval_(std::move(ev)) {
-        worker_ = std::thread([this] { run(); });
+        for (uint32_t k = 0; k < (workers ? workers : 1); k++) workers_.emplace_back([this, k] { run(k); });
     }
     ~BatchCore() { close(); }
 
@@ -87,7 +89,8 @@ class BatchCore {
         }
         cv_work_.notify_all();
         cv_room_.notify_all();
-        if (worker_.joinable()) worker_.join();
+        for (std::thread& t : workers_)
+            if (t.joinable()) t.join();
     }
 
     // blocking submit; returns the request's code
@@ -122,7 +125,7 @@ class BatchCore {
     }
 
    private:
-    void run() {
+    void run(uint32_t wid) {
         std::vector<BatchReq*> batch;
         for (;;) {
             batch.clear();
@@ -137,6 +140,7 @@ class BatchCore {
                     if (now >= flush_at) break;
                     cv_work_.wait_for(lock, std::chrono::nanoseconds(flush_at - now));
                 }
+                if (q_.empty()) continue;  // (another worker took them)
                 // up to max_batch requests of the oldest request's result shape
                 const uint32_t shape = q_.front()->n_out;
                 for (auto it = q_.begin(); it != q_.end() && batch.size() < max_batch_;) {
@@ -168,7 +172,7 @@ class BatchCore {
             // AuthConfig buckets (stable: arrival order inside a bucket)
             std::stable_sort(live.begin(), live.end(),
                              [](const BatchReq* a, const BatchReq* b) { return a->rs < b->rs; });
-            int rc = live.empty() ? kBatchOk : eval_(live);
+            int rc = live.empty() ? kBatchOk : eval_(live, wid);
             {  // counted before the callers wake, so a caller that returns sees its batch
                 std::lock_guard<std::mutex> lock(mu_);
                 if (!live.empty()) {
@@ -190,7 +194,7 @@ class BatchCore {
     std::deque<BatchReq*> q_;
     bool stopping_ = false;
     BatchStats stats_;
-    std::thread worker_;
+    std::vector<std::thread> workers_;
 };
 
 }  // namespace ajx

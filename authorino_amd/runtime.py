@@ -466,6 +466,27 @@ class Batcher:
         _check(rc, "authjx_batcher_eval")
         return list(tri), list(err)
 
+    def loadgen(self, rulesets, set_of_req, arena, offs, lens, threads: int = 64):
+        """Profiling: `threads` native producer threads push every request through this
+        batcher one blocking call at a time (authjx_debug_loadgen). Returns (per-request
+        latency ns, first result per request, wall ns)."""
+        L = load_library()
+        L.authjx_debug_loadgen.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+        n = len(lens)
+        sets = (C.c_void_p * len(rulesets))(*[r._h.value if isinstance(r._h, C.c_void_p) else r._h for r in rulesets])
+        sor = np.ascontiguousarray(set_of_req, dtype=np.uint32)
+        ar = np.ascontiguousarray(arena, dtype=np.uint8)
+        of = np.ascontiguousarray(offs, dtype=np.uint64)
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        lat = np.zeros(n, dtype=np.uint64)
+        tri = np.zeros(n, dtype=np.uint8)
+        wall = C.c_uint64()
+        _check(L.authjx_debug_loadgen(self._h, sets, sor.ctypes.data, ar.ctypes.data, of.ctypes.data, ln.ctypes.data,
+                                      n, threads, lat.ctypes.data, tri.ctypes.data, C.byref(wall)),
+               "authjx_debug_loadgen")
+        return lat, tri, wall.value
+
     def stats(self) -> Dict[str, int]:
         v = [C.c_uint64() for _ in range(4)]
         _check(load_library().authjx_batcher_stats(self._h, *[C.byref(x) for x in v]), "authjx_batcher_stats")

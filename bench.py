@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
+    ap.add_argument("--no-serve", action="store_true", help="skip the micro-batcher serving leg (c4)")
     ap.add_argument("--unique", type=int, default=None,
                     help="distinct document templates (default 16384 for c2/c3/c4, 4096 for c5)")
     ap.add_argument("--dry-run", action="store_true",
@@ -449,6 +450,29 @@ def main():
                                 "equal_to_restatement": bool(np.array_equal(got, w.set_of_req.astype(np.int32)))}
     undecided = int((tri_h == runtime.UNDECIDED).sum())
     exact_path = ctx.last_exact_count()  # requests the single-pass kernel handed to the exact scan
+    if rank == 0 and world == 1 and not args.no_serve and w.set_of_req is not None and nt == 1:
+        # the serving path (never the headline value): 64 native producer threads push a
+        # sample of the batch through the micro-batcher one blocking request at a time, as
+        # serving goroutines would (main.go:69,451; pkg/service/auth_pipeline.go:150-164)
+        extra["serving"] = []
+        for threads in (64, 256):  # (64 producers: the VERDICT's case; 256: a loaded server, within the box's task cap)
+            ns = min(w.n, 1 << 18)
+            b = runtime.Batcher(ctx, max_batch=8192, window_us=200)
+            try:
+                b.loadgen(rss, w.set_of_req[:4096], w.arena, w.offs[:4096], w.lens[:4096], threads=threads)  # (warm up)
+                b0 = b.stats()["batches"]
+                lat, stri, wall = b.loadgen(rss, w.set_of_req[:ns], w.arena, w.offs[:ns], w.lens[:ns], threads=threads)
+                st = b.stats()
+            finally:
+                b.close()
+            us = np.sort(lat.astype(np.float64) / 1e3)
+            extra["serving"].append({
+                "producer_threads": threads, "requests": int(ns), "decisions_per_s": ns / (wall * 1e-9),
+                "latency_us": {"p50": float(us[ns // 2]), "p99": float(us[int(ns * 0.99)]), "max": float(us[-1])},
+                "batches": st["batches"] - b0, "max_batch_seen": st["max_batch_seen"], "max_batch": 8192,
+                "window_us": 200, "workers": 2,
+                "equal_to_batch_results": bool(np.array_equal(stri, tri_h[:ns].astype(np.uint8))),
+                "note": "authjx_batcher_eval per request, blocking, from pageable host memory (H2D / D2H per batch)"})
 
     if rank == 0:
         line = {

@@ -24,7 +24,7 @@ extern "C" {
 void* hb_create(uint32_t max_batch, uint32_t window_us, uint32_t queue_cap, uint32_t delay_us) {
     Host* h = new Host();
     h->delay_us = delay_us;
-    h->core = new BatchCore(max_batch, (uint64_t)window_us * 1000ull, queue_cap, [h](std::vector<BatchReq*>& reqs) {
+    h->core = new BatchCore(max_batch, (uint64_t)window_us * 1000ull, queue_cap, [h](std::vector<BatchReq*>& reqs, uint32_t) {
         for (size_t i = 1; i < reqs.size(); i++) {
             if (reqs[i - 1]->rs > reqs[i]->rs) h->order_violations++;
             if (reqs[i]->n_out != reqs[0]->n_out) h->shape_violations++;
