@@ -441,8 +441,17 @@ int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* set
                                const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
                                const uint32_t* d_lens, uint32_t n, authjx_value* d_out_values,
                                uint32_t values_stride, void* stream) {
+    return authjx_select_text_batch_device(ctx, sets, n_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_values,
+                                           values_stride, nullptr, 0, stream);
+}
+
+int authjx_select_text_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                                    const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
+                                    const uint32_t* d_lens, uint32_t n, authjx_value* d_out_values,
+                                    uint32_t values_stride, uint8_t* d_out_text, uint32_t text_stride, void* stream) {
     if (!ctx || !sets || n_sets == 0 || (n && (!d_arena || !d_offs || !d_lens || !d_out_values)))
         return AUTHJX_EINVAL;
+    if (d_out_text && text_stride == 0) return AUTHJX_EINVAL;
     if (n_sets > 1 && !d_set_of_req) return AUTHJX_EINVAL;
     if (n_sets == 1) d_set_of_req = nullptr;
     uint32_t max_sel = 0;
@@ -476,7 +485,8 @@ int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* set
         (n_sets == 1 && sets[0]->c.blob.size() <= ajx::kMaxSharedBlobBytes) ? (uint32_t)sets[0]->c.blob.size() : 0u;
     HIP_OK(ajx::launch_select(w->d_sets, d_set_of_req, shared_bytes, d_arena, d_offs, d_lens, n,
                               reinterpret_cast<uint32_t*>(d_out_values), values_stride,
-                              exact ? nullptr : w->d_rows, row_stride, w->d_slow, w->d_slow + 1, perm, s));
+                              exact ? nullptr : w->d_rows, row_stride, w->d_slow, w->d_slow + 1, perm, d_out_text,
+                              text_stride, s));
     return batch_done(w, sets, n_sets);
 }
 
@@ -507,7 +517,16 @@ int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint
                         const uint32_t* set_of_req, const uint8_t* arena, uint64_t arena_len,
                         const uint64_t* offs, const uint32_t* lens, uint32_t n, authjx_value* out_values,
                         uint32_t values_stride) {
+    return authjx_select_text_batch(ctx, sets, n_sets, set_of_req, arena, arena_len, offs, lens, n, out_values,
+                                    values_stride, nullptr, 0);
+}
+
+int authjx_select_text_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                             const uint32_t* set_of_req, const uint8_t* arena, uint64_t arena_len,
+                             const uint64_t* offs, const uint32_t* lens, uint32_t n, authjx_value* out_values,
+                             uint32_t values_stride, uint8_t* out_text, uint32_t text_stride) {
     if (!ctx || (n && (!arena || !offs || !lens || !out_values))) return AUTHJX_EINVAL;
+    if (out_text && text_stride == 0) return AUTHJX_EINVAL;
     for (uint32_t r = 0; r < n; r++)
         if (offs[r] + lens[r] > arena_len || (set_of_req && set_of_req[r] >= n_sets)) return AUTHJX_EINVAL;
     const bool with_sor = set_of_req != nullptr;
@@ -516,7 +535,9 @@ int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint
     const size_t o_sor = round_up(o_lens + (size_t)n * 4, 256);
     const size_t o_out = round_up(o_sor + (with_sor ? (size_t)n * 4 : 0), 256);
     const size_t out_bytes = (size_t)n * values_stride * sizeof(authjx_value);
-    const size_t total = round_up(o_out + out_bytes, 256);
+    const size_t o_text = round_up(o_out + out_bytes, 256);
+    const size_t text_bytes = out_text ? (size_t)n * text_stride : 0;
+    const size_t total = round_up(o_text + text_bytes, 256);
     std::lock_guard<std::mutex> batch_lock(ctx->batch_mu);
     {
         HIP_OK(hipSetDevice(ctx->device));
@@ -536,11 +557,13 @@ int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint
         if (with_sor) HIP_OK(hipMemcpyAsync(b + o_sor, set_of_req, (size_t)n * 4, hipMemcpyHostToDevice, s));
     }
     uint8_t* b = ctx->d_stage;
-    int rc = authjx_select_batch_device(ctx, sets, n_sets, with_sor ? (const uint32_t*)(b + o_sor) : nullptr, b,
-                                        (const uint64_t*)(b + o_offs), (const uint32_t*)(b + o_lens), n,
-                                        (authjx_value*)(b + o_out), values_stride, nullptr);
+    int rc = authjx_select_text_batch_device(ctx, sets, n_sets, with_sor ? (const uint32_t*)(b + o_sor) : nullptr,
+                                             b, (const uint64_t*)(b + o_offs), (const uint32_t*)(b + o_lens), n,
+                                             (authjx_value*)(b + o_out), values_stride,
+                                             out_text ? b + o_text : nullptr, text_stride, nullptr);
     if (rc != AUTHJX_OK) return rc;
     HIP_OK(hipMemcpyAsync(out_values, b + o_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (out_text) HIP_OK(hipMemcpyAsync(out_text, b + o_text, text_bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_OK(hipStreamSynchronize(ctx->stream));
     return AUTHJX_OK;
 }

@@ -16,7 +16,8 @@ hipError_t launch_eval_scan(const uint8_t* const* d_sets, const uint32_t* d_set_
 hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
                          const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                          uint32_t* d_out, uint32_t stride, uint64_t* d_rows, uint32_t row_stride,
-                         uint32_t* d_slow_count, uint32_t* d_slow_ids, const uint32_t* d_perm, hipStream_t stream);
+                         uint32_t* d_slow_count, uint32_t* d_slow_ids, const uint32_t* d_perm, uint8_t* d_text,
+                         uint32_t text_stride, hipStream_t stream);
 
 // The values of patterns [p0, p0 + stride) of sets[0] from capture rows an earlier
 // single-pass evaluation of that ruleset wrote (no document scan; slow rows: exact Get).

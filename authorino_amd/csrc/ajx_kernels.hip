@@ -624,8 +624,11 @@ hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist
 // gjson.Get per pattern selector (the response / header selectors of SURVEY.md §8 a14):
 // one work-item per request, the exact device Get (gj_get) for each of the ruleset's
 // patterns; out[r * stride + p] = {start (relative to the document), len, type, esc}.
-// An UNSUPPORTED selector, and one with modifiers (its value is not a span of the
-// document), reports type 0xFF.
+// An UNSUPPORTED selector reports type 0xFF. TEXT: a selector with modifiers and a "#."
+// list resolve to built text, copied into the request's slot text[r * text_stride ...]
+// (select_value, ajx_modifiers.h; 0xFF when it does not fit); without TEXT they report
+// 0xFF (the capture-row path of select_from_eval).
+template <bool TEXT>
 __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* __restrict__ sets,
                                                          const uint32_t* __restrict__ set_of_req,
                                                          const uint8_t* __restrict__ arena,
@@ -634,7 +637,8 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
                                                          uint32_t* __restrict__ out, uint32_t stride,
                                                          const uint64_t* __restrict__ rows, uint32_t row_stride,
                                                          uint32_t p0, const uint32_t* __restrict__ perm,
-                                                         uint32_t wave_rows) {
+                                                         uint32_t wave_rows, uint8_t* __restrict__ text,
+                                                         uint32_t text_stride) {
     // work-item k: request perm[k] (the order the rows were written in) or k; its row is
     // row k of the wave-interleaved layout (wave_rows: the fused kernels') or row r
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -656,16 +660,25 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
     // evaluation, the response selectors compiled as its last tree
     const uint32_t avail = h->n_patterns > p0 ? h->n_patterns - p0 : 0u;
     const uint32_t np = avail < stride ? avail : stride;
+    [[maybe_unused]] uint32_t used = 0;  // (TEXT: bytes of the request's text slot taken)
     for (uint32_t q = 0; q < np; q++) {
         const uint32_t p = p0 + q;
         uint32_t* o = out + ((size_t)r * stride + q) * 3;
-        if (pats[p].state == P_UNSUPPORTED || sels[pats[p].selector].mod_count) {
+        const uint32_t si = pats[p].selector;
+        if (pats[p].state == P_UNSUPPORTED || (!TEXT && sels[si].mod_count)) {
             o[0] = 0;
             o[1] = 0;
             o[2] = 0xFFu;
             continue;
         }
-        const uint32_t si = pats[p].selector;
+        if constexpr (TEXT) {
+            if (sels[si].mod_count) {
+                ModBufs mb;
+                if (!select_value(blob, sels[si], doc, len, mb, text + (size_t)r * text_stride, text_stride, &used, o))
+                    o[0] = 0, o[1] = 0, o[2] = 0xFFu;
+                continue;
+            }
+        }
         if (!(found & kRowSlow)) {
             if ((found >> si) & 1u) {
                 const uint64_t rec = row[1 + si];
@@ -684,15 +697,23 @@ __global__ __launch_bounds__(256) void ajx_select_values(const uint8_t* const* _
         const ValueRef v = gj_get(doc, len, comps + sl.comp_begin, sl.comp_count, lits);
         o[0] = v.start;
         o[1] = v.end - v.start;
-        // (a "#." list is a built text, not a document span: not selectable)
-        o[2] = v.esc == kValList ? 255u : (uint32_t)v.type | ((uint32_t)v.esc << 8);
+        o[2] = (uint32_t)v.type | ((uint32_t)v.esc << 8);
+        if (v.esc == kValList) {  // a "#." list: built text (without TEXT: not selectable)
+            o[2] = 0xFFu;
+            if constexpr (TEXT) {
+                ModBufs mb;
+                if (!select_value(blob, sl, doc, len, mb, text + (size_t)r * text_stride, text_stride, &used, o))
+                    o[0] = 0, o[1] = 0, o[2] = 0xFFu;
+            }
+        }
     }
 }
 
 hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t shared_blob_bytes,
                          const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                          uint32_t* d_out, uint32_t stride, uint64_t* d_rows, uint32_t row_stride,
-                         uint32_t* d_slow_count, uint32_t* d_slow_ids, const uint32_t* d_perm, hipStream_t stream) {
+                         uint32_t* d_slow_count, uint32_t* d_slow_ids, const uint32_t* d_perm, uint8_t* d_text,
+                         uint32_t text_stride, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     if (d_rows) {  // stage A of the single-pass kernel captures every selector's span
         const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
@@ -725,8 +746,12 @@ hipError_t launch_select(const uint8_t* const* d_sets, const uint32_t* d_set_of_
     }
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
-    hipLaunchKernelGGL(ajx_select_values, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena, d_offs,
-                       d_lens, n, d_out, stride, d_rows, row_stride, 0u, nullptr, 0u);
+    if (d_text)
+        hipLaunchKernelGGL(ajx_select_values<true>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, n, d_out, stride, d_rows, row_stride, 0u, nullptr, 0u, d_text, text_stride);
+    else
+        hipLaunchKernelGGL(ajx_select_values<false>, dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, n, d_out, stride, d_rows, row_stride, 0u, nullptr, 0u, nullptr, 0u);
     return hipGetLastError();
 }
 
@@ -737,8 +762,8 @@ hipError_t launch_select_rows(const uint8_t* const* d_sets, const uint8_t* d_are
     if (n == 0) return hipSuccess;
     const uint32_t block = 256;
     const uint32_t grid = (n + block - 1) / block;
-    hipLaunchKernelGGL(ajx_select_values, dim3(grid), dim3(block), 0, stream, d_sets, nullptr, d_arena, d_offs,
-                       d_lens, n, d_out, stride, d_rows, row_stride, p0, d_perm, wave_rows ? 1u : 0u);
+    hipLaunchKernelGGL(ajx_select_values<false>, dim3(grid), dim3(block), 0, stream, d_sets, nullptr, d_arena, d_offs,
+                       d_lens, n, d_out, stride, d_rows, row_stride, p0, d_perm, wave_rows ? 1u : 0u, nullptr, 0u);
     return hipGetLastError();
 }
 

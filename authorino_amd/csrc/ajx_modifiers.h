@@ -420,4 +420,43 @@ AJX_HD bool apply_modifiers(const uint8_t* blob, const Selector& sel, const uint
     return mod_parse(in, in_n, mb.t, rdoc, rv);
 }
 
+// authjx_value.esc flag of a value that is built text (a modifier chain's output, a "#."
+// list), not a span of the document: [start, start + len) of the request's text slot
+constexpr uint8_t kValText = 4;
+
+// The value of selector `sl` as JSONValue.ResolveFor / ReplaceJSONPlaceholders see it
+// (pkg/json/json.go:41-53, :96-151: gjson.Get with the path's modifiers): a span of the
+// document, or, after a modifier chain or for a "#." list, the final Result's raw text
+// appended to the request's text slot text[*used, cap) (esc | kValText). out = {start,
+// len, type | esc << 8}. False when undecided (the slot or a buffer is full, Unicode case
+// mapping, ...).
+AJX_HD bool select_value(const uint8_t* blob, const Selector& sl, const uint8_t* doc, uint32_t len, ModBufs& mb,
+                         uint8_t* text, uint32_t cap, uint32_t* used, uint32_t* out) {
+    const RulesetHdr* h = (const RulesetHdr*)blob;
+    const Component* comps = (const Component*)(blob + h->off_components);
+    const uint8_t* lits = blob + h->off_literals;
+    const ValueRef v = gj_get(doc, len, comps + sl.comp_begin, sl.comp_count, lits);
+    const uint8_t* rd = doc;
+    ValueRef rv = v;
+    if (v.esc == kValList) {  // (a "#." list has no modifier chain after it)
+        if (!build_list(blob, sl, doc, v, mb, &rd, &rv)) return false;
+    } else if (sl.mod_count) {
+        if (!apply_modifiers(blob, sl, doc, v, mb, &rd, &rv)) return false;
+    }
+    if (rd == doc) {  // the document's own span (or a count, or Null)
+        out[0] = rv.start;
+        out[1] = rv.end - rv.start;
+        out[2] = (uint32_t)rv.type | ((uint32_t)rv.esc << 8);
+        return true;
+    }
+    const uint32_t n = rv.end - rv.start;
+    if (!text || n > cap - *used) return false;
+    for (uint32_t i = 0; i < n; i++) text[*used + i] = rd[rv.start + i];
+    out[0] = *used;
+    out[1] = n;
+    out[2] = (uint32_t)rv.type | ((uint32_t)(rv.esc | kValText) << 8);
+    *used += n;
+    return true;
+}
+
 }  // namespace ajx

@@ -319,8 +319,8 @@ class AuthPipelineBatch:
             self._responses(results, docs, live, arena, offs, lens)
         return results
 
-    def _spans(self, sel: ValueSelectors, docs, idx) -> np.ndarray:
-        """The selector spans of docs[idx] (one device select launch)."""
+    def _spans(self, sel: ValueSelectors, docs, idx):
+        """The selector values of docs[idx] (one device select launch)."""
         sub = [docs[i] for i in np.asarray(idx).tolist()]
         lens = np.fromiter((len(d) for d in sub), dtype=np.uint32, count=len(sub))
         offs = np.zeros(len(sub), dtype=np.uint64)
@@ -331,9 +331,10 @@ class AuthPipelineBatch:
 
     @staticmethod
     def _set_aside_spans(spans, idx, results) -> np.ndarray:
-        """Requests whose selector spans the device left unresolved (type 255) become
-        undecided; returns that mask over idx."""
-        und = ((spans[:, :, 2] & 0xFF) == 255).any(axis=1) if spans.size else np.zeros(len(idx), dtype=bool)
+        """Requests whose selector values the device left unresolved (type 255: a value
+        over its text slot, non-ASCII @case / @strip) become undecided; returns that mask
+        over idx."""
+        und = spans.unresolved()
         for i in np.asarray(idx)[und].tolist():
             results[i].undecided = True
             results[i].code = CODE_UNKNOWN
@@ -375,7 +376,7 @@ class AuthPipelineBatch:
         offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
         arena = np.frombuffer(b"".join(sub) + b"\0", dtype=np.uint8)
         spans = self.selectors.resolve(sub, arena, offs, lens)
-        if spans.size and ((spans[:, :, 2] & 0xFF) == 255).any():
+        if spans.unresolved().any():
             raise runtime.AuthjxError("device could not resolve a response selector")
         granted = [dict() for _ in sub]
         idx = np.arange(len(sub))

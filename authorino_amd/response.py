@@ -186,6 +186,47 @@ def _go_bytes_str(b: bytes) -> str:
 # authjx_value.esc of an element count (a `#` path part; ajx_device.h kValCount): the
 # count is in `start`, not a document span
 VAL_COUNT = 2
+# authjx_value.esc flag of built text (a modifier chain's or a "#." list's Result;
+# ajx_modifiers.h kValText): [start, start + len) of the request's text slot
+VAL_TEXT = 4
+
+
+class SelectedRow:
+    """One request's selected values: spans[k] = {start, len, type | esc << 8} and the text
+    slot that VAL_TEXT values point into."""
+
+    __slots__ = ("spans", "text")
+
+    def __init__(self, spans, text=None):
+        self.spans, self.text = spans, text
+
+    def __getitem__(self, k):
+        return self.spans[k]
+
+    def source(self, t: int, doc: bytes) -> bytes:
+        if (int(t) >> 8) & VAL_TEXT:
+            return self.text.tobytes()
+        return doc
+
+
+class Selected:
+    """ValueSelectors.resolve's output for n requests: spans u32[n][k][3] and text slots
+    u8[n][text_stride] (authjx_select_text_batch)."""
+
+    def __init__(self, spans: np.ndarray, text: Optional[np.ndarray] = None):
+        self.spans, self.text = spans, text
+
+    def __len__(self):
+        return len(self.spans)
+
+    def __getitem__(self, j) -> SelectedRow:
+        return SelectedRow(self.spans[j], None if self.text is None else self.text[j])
+
+    def unresolved(self) -> np.ndarray:
+        """Requests with a value the device left unresolved (type 255)."""
+        if not self.spans.size:
+            return np.zeros(len(self.spans), dtype=bool)
+        return ((self.spans[:, :, 2] & 0xFF) == 255).any(axis=1)
 
 
 def result_string(doc: bytes, start: int, length: int, typ: int) -> str:
@@ -509,22 +550,31 @@ class ValueSelectors:
         if self.paths:
             pats = [(p, int(jsonexp.EqualOperator), "") for p in self.paths]
             self.ruleset = ctx.compile(pats, [], -1)
-            # (a "#." list is a built JSON text, not a document span: not selectable)
-            bad = [p for p, st in zip(self.paths, self.ruleset.status)
-                   if st != 0 or re.search(r"(^|(?<!\\)\.)#\.", p)]
+            bad = [p for p, st in zip(self.paths, self.ruleset.status) if st != 0]
             if bad:
                 from .runtime import AuthjxError
 
                 raise AuthjxError(f"{what} not compiled for the device: {bad}")
 
-    def resolve(self, docs: Sequence[bytes], arena, offs, lens) -> np.ndarray:
-        """u32[n][n_paths][3] spans {start, len, type | esc << 8} from the device."""
+    # bytes of built text per request (modifier chains, "#." lists); a request whose
+    # values do not fit is left undecided
+    TEXT_STRIDE = 8192
+
+    def resolve(self, docs: Sequence[bytes], arena, offs, lens) -> Selected:
+        """The values of every path for each request from the device: spans {start, len,
+        type | esc << 8} of the document or of the request's text slot (VAL_TEXT)."""
         if self.ruleset is None:
-            return np.zeros((len(docs), 0, 3), dtype=np.uint32)
-        return self.ctx.select_host_arena([self.ruleset], arena, offs, lens)
+            return Selected(np.zeros((len(docs), 0, 3), dtype=np.uint32))
+        spans, text = self.ctx.select_text_host_arena([self.ruleset], arena, offs, lens,
+                                                      text_stride=self.TEXT_STRIDE)
+        return Selected(spans, text)
 
     def value(self, v: JSONValue, doc: bytes, spans_r) -> object:
         return self._value(v, doc, spans_r)
+
+    @staticmethod
+    def _src(spans_r, t, doc: bytes) -> bytes:
+        return spans_r.source(t, doc) if isinstance(spans_r, SelectedRow) else doc
 
     def _value(self, v: JSONValue, doc: bytes, spans_r) -> object:
         if not v.pattern:
@@ -539,12 +589,12 @@ class ValueSelectors:
                     if int(t) >> 8 == VAL_COUNT:
                         parts.append(str(int(st)))
                     else:
-                        parts.append(result_string(doc, int(st), int(ln), int(t) & 0xFF))
+                        parts.append(result_string(self._src(spans_r, t, doc), int(st), int(ln), int(t) & 0xFF))
             return "".join(parts)
         st, ln, t = spans_r[self._slot[v.pattern]]
         if int(t) >> 8 == VAL_COUNT:  # an array's element count (a `#` part): Number
             return float(int(st))
-        return result_value(doc, int(st), int(ln), int(t) & 0xFF)
+        return result_value(self._src(spans_r, t, doc), int(st), int(ln), int(t) & 0xFF)
 
 
 class ResponseSelectors(ValueSelectors):

@@ -49,7 +49,7 @@ EXPORTS = [
     "authjx_ruleset_patterns", "authjx_ruleset_selectors", "authjx_pattern_error",
     "authjx_eval_batch_device", "authjx_eval_batch", "authjx_last_kernel_ms", "authjx_set_exact_scan",
     "authjx_last_exact_count", "authjx_select_batch_device", "authjx_select_batch", "authjx_compile_forest",
-    "authjx_select_from_eval_device",
+    "authjx_select_from_eval_device", "authjx_select_text_batch_device", "authjx_select_text_batch",
     "authjx_ruleset_trees", "authjx_batcher_create", "authjx_batcher_destroy", "authjx_batcher_eval",
     "authjx_batcher_stats",
     "authjx_index_new", "authjx_index_free", "authjx_index_set", "authjx_index_delete_key", "authjx_index_get",
@@ -131,6 +131,14 @@ def load_library(path: str = LIB_PATH):
             C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
             C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
         L.authjx_select_batch.restype = C.c_int
+        L.authjx_select_text_batch_device.argtypes = [
+            C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+            C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]
+        L.authjx_select_text_batch_device.restype = C.c_int
+        L.authjx_select_text_batch.argtypes = [
+            C.c_void_p, C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+            C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
+        L.authjx_select_text_batch.restype = C.c_int
         L.authjx_last_kernel_ms.argtypes = [C.c_void_p]
         L.authjx_last_kernel_ms.restype = C.c_float
         L.authjx_set_exact_scan.argtypes = [C.c_void_p, C.c_int]
@@ -300,6 +308,42 @@ class Context:
             self._h, rs._h, int(first_pattern), ptr(arena), ptr(offs), ptr(lens), n, ptr(out), int(out.shape[1]),
             C.c_void_p(stream) if stream else None)
         _check(rc, "authjx_select_from_eval_device")
+
+    def select_text_device(self, sets, arena, offs, lens, out, text, set_of_req=None, stream=None) -> None:
+        """authjx_select_text_batch_device: select_device plus modifier chains and "#." lists,
+        whose values are built text in text[r] (u8[n][text_stride]). Asynchronous."""
+        n = int(lens.numel())
+        sarr = (C.c_void_p * len(sets))(*[s._h.value for s in sets])
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        rc = load_library().authjx_select_text_batch_device(
+            self._h, sarr, len(sets), ptr(set_of_req), ptr(arena), ptr(offs), ptr(lens), n, ptr(out),
+            int(out.shape[1]), ptr(text), int(text.shape[1]), C.c_void_p(stream) if stream else None)
+        _check(rc, "authjx_select_text_batch_device")
+
+    def select_text_host_arena(self, sets, arena, offs, lens, set_of_req=None, text_stride: int = 4096):
+        """authjx_select_text_batch: (u32[n][stride][3] values, u8[n][text_stride] text
+        slots); a value whose esc has VALUE_TEXT is [start, start + len) of its request's
+        slot (a modifier chain's / "#." list's Result), else a span of the document."""
+        n = int(lens.shape[0])
+        stride = max(1, max(s.n_patterns for s in sets))
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        if arena.nbytes == 0:
+            arena = np.zeros(1, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.zeros((max(n, 1), stride, 3), dtype=np.uint32)
+        text = np.zeros((max(n, 1), text_stride), dtype=np.uint8)
+        sor = None
+        if set_of_req is not None:
+            set_of_req = np.ascontiguousarray(set_of_req, dtype=np.uint32)
+            sor = C.c_void_p(set_of_req.ctypes.data)
+        sarr = (C.c_void_p * len(sets))(*[s._h.value for s in sets])
+        rc = load_library().authjx_select_text_batch(
+            self._h, sarr, len(sets), sor, C.c_void_p(arena.ctypes.data), int(arena.nbytes),
+            C.c_void_p(offs.ctypes.data), C.c_void_p(lens.ctypes.data), n, C.c_void_p(out.ctypes.data), stride,
+            C.c_void_p(text.ctypes.data), text_stride)
+        _check(rc, "authjx_select_text_batch")
+        return out[:n], text[:n]
 
     def select_host_arena(self, sets, arena, offs, lens, set_of_req=None) -> np.ndarray:
         """gjson.Get of every pattern selector of each request's ruleset on the device

@@ -200,6 +200,10 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
 #define AUTHJX_JSON_UNSUPPORTED 255
 #define AUTHJX_VALUE_COUNT 2 /* authjx_value.esc: `start` is an array's element count (a
                               * last path part "#", gjson parseArray), len 0: no span */
+#define AUTHJX_VALUE_TEXT 4  /* authjx_value.esc flag (with 1 = escapes): the value is built
+                              * text — the Result of a modifier chain or a "#." list — at
+                              * [start, start + len) of the request's text slot
+                              * (authjx_select_text_batch[_device]) */
 typedef struct {
     uint32_t start;
     uint32_t len;
@@ -233,6 +237,22 @@ int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint
                         const uint32_t* set_of_req, const uint8_t* arena, uint64_t arena_len,
                         const uint64_t* offs, const uint32_t* lens, uint32_t n, authjx_value* out_values,
                         uint32_t values_stride);
+/* authjx_select_batch[_device] for selectors with gjson modifiers (`a.b|@case:upper`,
+ * `@extract:{...}`, ...) and "#." lists: their values are built text, not document spans
+ * — the response / denyWith / cache-key templates of pkg/json/json.go:96-151 and
+ * pkg/evaluators/authorization.go:56-66. Request r's text slot is
+ * out_text[r * text_stride, (r + 1) * text_stride); a value esc has AUTHJX_VALUE_TEXT and
+ * start / len within that slot. A value that does not fit, or that the device leaves
+ * undecided (non-ASCII @case / @strip), is AUTHJX_JSON_UNSUPPORTED. Plain selectors are
+ * document spans as above. */
+int authjx_select_text_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                                    const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
+                                    const uint32_t* d_lens, uint32_t n, authjx_value* d_out_values,
+                                    uint32_t values_stride, uint8_t* d_out_text, uint32_t text_stride, void* stream);
+int authjx_select_text_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                             const uint32_t* set_of_req, const uint8_t* arena, uint64_t arena_len,
+                             const uint64_t* offs, const uint32_t* lens, uint32_t n, authjx_value* out_values,
+                             uint32_t values_stride, uint8_t* out_text, uint32_t text_stride);
 
 /* Route every request through the exact per-selector scan kernel instead of the
  * single-pass kernel (results are identical; used to cross-check the two paths). */

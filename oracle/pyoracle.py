@@ -144,6 +144,25 @@ def gjson_string_mods(doc, path):
     return out
 
 
+def gjson_get_mods(doc, path):
+    """(type, raw) of gjson.Get(doc, path) with the path's modifiers (gjson_mods_ref.c);
+    None when undecided (non-ASCII text under @case / @strip)."""
+    L = lib()
+    d, p = _b(doc), _b(path)
+    r = _Result()
+    text = _Buf()
+    rc = L.or_gjson_get_mods(d, len(d), p, len(p), C.byref(r), C.byref(text))
+    if rc == -1:
+        L.or_buf_free(C.byref(text))
+        raise ValueError(f"oracle: unsupported selector {path!r}")
+    out = None
+    if rc == 0:
+        out = (r.type, C.string_at(r.raw, r.raw_len) if r.raw_len else b"")
+    L.or_result_free(C.byref(r))
+    L.or_buf_free(C.byref(text))
+    return out
+
+
 def gjson_span(doc, path) -> Tuple[int, int, int]:
     """-> (type, start, length): gjson.Get's Raw as a span of the document"""
     L = lib()

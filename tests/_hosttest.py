@@ -38,6 +38,9 @@ def lib():
         L.ht_get.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ht_get.restype = C.c_int
         L.ht_string.argtypes = [C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32]
+        L.ht_select_value.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_void_p, C.c_uint32,
+                                      C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.ht_select_value.restype = C.c_int
         L.ht_string.restype = C.c_int
         L.ht_regex.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
         L.ht_regex.restype = C.c_void_p
@@ -92,6 +95,16 @@ class HostRuleset:
         err = C.c_int32(-1)
         t = lib().ht_eval(self._h, d, len(d), res, C.byref(err))
         return t, err.value, list(res)[: self.n]
+
+    def select_value(self, p, doc, text, used):
+        """select_value of pattern p's selector (the select kernel's TEXT instance): (rc,
+        [start, len, type | esc << 8], used) with built text appended to `text` (bytearray)."""
+        d = _b(doc)
+        buf = (C.c_uint8 * len(text)).from_buffer(text)
+        u = C.c_uint32(used)
+        out = (C.c_uint32 * 3)()
+        rc = lib().ht_select_value(self._h, p, d, len(d), buf, len(text), C.byref(u), out)
+        return rc, list(out), u.value
 
     def __del__(self):
         if getattr(self, "_h", None):

@@ -77,6 +77,21 @@ int ht_eval(void* h, const uint8_t* doc_in, uint32_t len, uint8_t* res, int32_t*
     return run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
 }
 
+// select_value (ajx_modifiers.h): the value of pattern p's selector as the select kernel
+// resolves it with a text slot; returns 0, or -1 undecided (out = {start, len, type | esc << 8})
+int ht_select_value(void* h, uint32_t p, const uint8_t* doc_in, uint32_t len, uint8_t* text, uint32_t cap,
+                    uint32_t* used, uint32_t* out) {
+    std::vector<uint8_t> buf(len + 32, 0);
+    uint8_t* doc = buf.data() + 16;
+    if (len) std::memcpy(doc, doc_in, len);
+    const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
+    const RulesetHdr* hd = (const RulesetHdr*)blob;
+    const Selector* sels = (const Selector*)(blob + hd->off_selectors);
+    const Pattern* pats = (const Pattern*)(blob + hd->off_patterns);
+    static ModBufs mb;
+    return select_value(blob, sels[pats[p].selector], doc, len, mb, text, cap, used, out) ? 0 : -1;
+}
+
 // value resolution only: type + raw span
 int ht_get(const char* path, uint32_t plen, const uint8_t* doc_in, uint32_t len, uint32_t* start, uint32_t* end) {
     std::vector<uint8_t> buf(len + 32, 0);

@@ -60,18 +60,31 @@ def test_deny_with_selectors_and_stringify():
     assert res[1].deny_headers[2] == {"X-Who": "carol@zeta"}
 
 
-def test_modifier_value_selectors_leave_request_undecided():
-    """A denyWith / cache-key selector with gjson modifiers has no document span to hand
-    back (the select kernel reports 0xFF): the request is set aside as undecided (the
-    evaluator's own host path resolves it), never answered with the unmodified value."""
-    dw = P.DenyWithValues(message=JSONValue(pattern="auth.identity.tenant.@case:upper"))
+def test_modifier_value_selectors_resolve_to_built_text():
+    """denyWith / cache-key selectors with the reference's modifiers and "#." lists
+    (json.go:96-151, :161-264): their values are the modifier chain's Result (built text
+    in the request's select text slot, AUTHJX_VALUE_TEXT), never the unmodified value; a
+    value the device cannot build (non-ASCII @case) leaves that request undecided."""
+    dw = P.DenyWithValues(message=JSONValue(pattern="auth.identity.tenant.@case:upper"),
+                          body=JSONValue(pattern='{auth.identity.sub|@extract:{"sep":"i","pos":0}}-{auth.identity.roles.#.x}'),
+                          headers=[("X-Roles", JSONValue(pattern="auth.identity.roles|@case:upper"))])
     cfg = P.AuthConfig(authorization=[_deny_all()], unauthorized=dw)
-    (r,) = P.AuthPipelineBatch(cfg, ctx=OracleCtx()).evaluate([_req()])
-    assert r.undecided and r.code == P.CODE_UNKNOWN
-    cached = P.AuthorizationConfig("c", rules=J.All(),
-                                   cache=CA.EvaluatorCache(JSONValue(pattern="auth.identity.sub|@reverse"), 60))
-    res = P.AuthPipelineBatch(P.AuthConfig(authorization=[cached]), ctx=OracleCtx()).evaluate([_req(), _req()])
-    assert all(r.undecided and not r.authorization for r in res)
+    raw_tenant = _req(sub="bob", tenant="zeta").replace(b'"zeta"', '"zéta"'.encode())  # (raw UTF-8)
+    res = P.AuthPipelineBatch(cfg, ctx=OracleCtx()).evaluate([_req(), raw_tenant])
+    r = res[0]
+    assert not r.undecided and r.code == P.CODE_PERMISSION_DENIED
+    assert r.message == "ACME" and r.body == "al-[]"
+    assert r.deny_headers == [{"X-Roles": '["USER"]'}]
+    assert res[1].undecided and res[1].code == P.CODE_UNKNOWN  # (Unicode case mapping)
+    # a cache key through a modifier: requests with the same key after @case:lower share
+    # the cached decision (authorization.go:59-74)
+    cached = P.AuthorizationConfig(
+        "c", rules=J.All(J.Pattern("auth.identity.sub", J.EqualOperator, "alice")),
+        cache=CA.EvaluatorCache(JSONValue(pattern="{auth.identity.tenant|@case:lower}/{auth.identity.sub}"), 60))
+    b = P.AuthPipelineBatch(P.AuthConfig(authorization=[cached]), ctx=OracleCtx())
+    first = b.evaluate([_req(tenant="ACME")])
+    assert first[0].code == P.CODE_OK and not first[0].undecided
+    assert cached.cache.get("acme/alice") is True
 
 
 def test_deny_with_only_on_denied_requests():

@@ -86,3 +86,65 @@ def test_modifier_chains_match_oracle(seed):
             assert res == [1, 0], (sel, d, w, res)
             checked += 1
     assert checked > 300 and undecided <= checked // 5, (checked, undecided)
+
+
+def _check_select(hr, p, d, want, text):
+    rc, out, used = hr.select_value(p, d, text, 0)
+    if rc != 0:
+        return False
+    st, ln, tt = out
+    src = bytes(text) if (tt >> 8) & 4 else d  # (AUTHJX_VALUE_TEXT: the request's text slot)
+    t, raw = want
+    assert (tt & 0xFF, src[st:st + ln]) == (t, raw), (d, out)
+    return True
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_select_value_text_matches_oracle(seed):
+    """The select kernel's value of a modifier-chain selector (select_value, host build):
+    the final Result's type and raw text, copied into the request's text slot, equal the
+    oracle's gjson.Get with the same modifiers (json.go:96-151 ReplaceJSONPlaceholders)."""
+    rng = random.Random(1900 + seed)
+    checked = undecided = 0
+    for _ in range(200):
+        sel = _chain(rng)
+        hr = None
+        for _ in range(3):
+            d = _doc(rng)
+            try:
+                want = O.gjson_get_mods(d, sel)
+            except ValueError:
+                break
+            if hr is None:
+                hr = H.HostRuleset([(sel, 1, "")], [(0, -1, -1, 0)], 0)
+                assert hr.status == [0], sel
+            if want is None:
+                continue
+            if _check_select(hr, 0, d, want, bytearray(4096)):
+                checked += 1
+            else:
+                undecided += 1
+    assert checked > 300 and undecided <= checked // 5, (checked, undecided)
+
+
+def test_select_value_lists_and_slot_overflow():
+    """"#." lists as built text; several built values share one slot (offsets advance);
+    a value larger than what is left of the slot is undecided."""
+    d = b'{"a":[{"k":"x"},{"k":2},{"j":1},{"k":[1,{"z":"q"}]}],"s":"abc","e":[]}'
+    pats = [("a.#.k", 1, ""), ("s|@case:upper", 1, ""), ("e.#.k", 1, ""), ("s", 1, "")]
+    hr = H.HostRuleset(pats, [(0, -1, -1, i) for i in range(4)] + [(1, 0, 1, -1), (1, 4, 2, -1), (1, 5, 3, -1)], 6)
+    text = bytearray(64)
+    used = 0
+    got = []
+    for p, (sel, _, _) in enumerate(pats):
+        rc, out, used = hr.select_value(p, d, text, used)
+        assert rc == 0
+        got.append(out)
+        st, ln, tt = out
+        src = bytes(text) if (tt >> 8) & 4 else d
+        t, raw, _ = O.gjson_get(d, sel) if "@" not in sel else (*O.gjson_get_mods(d, sel), None)
+        assert (tt & 0xFF, src[st:st + ln]) == (t, raw), sel
+    assert got[1][0] == got[0][1] and got[3][2] >> 8 == 0  # (the second built value follows the first)
+    small = bytearray(8)
+    rc, _, _ = hr.select_value(0, d, small, 0)
+    assert rc == -1

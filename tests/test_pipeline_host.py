@@ -8,6 +8,7 @@ Cases follow pkg/service/auth_pipeline_test.go:389-495 (conditions at AuthConfig
 evaluator level), pkg/evaluators/authorization/json_test.go (Unauthorized / regex error)
 and controllers/auth_config_controller.go:805-852 (tree order)."""
 import json
+import re
 
 import numpy as np
 import pytest
@@ -73,6 +74,34 @@ class OracleCtx:
                     t, st, ln = 255, 0, 0
                 out[r, p] = (st, ln, t)
         return out
+
+    def select_text_host_arena(self, sets, arena, offs, lens, set_of_req=None, text_stride=4096):
+        """authjx_select_text_batch's contract: document spans, or (modifier chains, "#."
+        lists) the oracle's raw Result text in the request's slot, esc | VALUE_TEXT."""
+        n = len(lens)
+        out = np.zeros((n, max(s.n_patterns for s in sets), 3), dtype=np.uint32)
+        text = np.zeros((n, text_stride), dtype=np.uint8)
+        for r in range(n):
+            doc = arena[int(offs[r]):int(offs[r]) + int(lens[r])].tobytes()
+            used = 0
+            for p, path in enumerate(sets[0 if set_of_req is None else int(set_of_req[r])].paths):
+                if "@" not in path and not re.search(r"(^|(?<!\\)\.)#\.", path):
+                    t, st, ln = O.gjson_span(doc, path)
+                    out[r, p] = (st, ln, t)
+                    continue
+                got = O.gjson_get_mods(doc, path)
+                if got is None or used + len(got[1]) > text_stride:
+                    out[r, p] = (0, 0, 255)
+                    continue
+                t, raw = got
+                if not raw:  # (Null: no text)
+                    out[r, p] = (0, 0, t)
+                    continue
+                text[r, used:used + len(raw)] = np.frombuffer(raw, dtype=np.uint8)
+                esc = (1 if t == 3 and b"\\" in raw else 0) | 4
+                out[r, p] = (used, len(raw), t | esc << 8)
+                used += len(raw)
+        return out, text
 
     def eval_host_arena(self, sets, arena, offs, lens, set_of_req=None, with_bitmap=True):
         self.launches += 1

@@ -109,6 +109,21 @@ def test_replace_json_placeholders():
         assert "".join(out) == want, tpl
         if R.JSONValue(pattern=tpl).is_template() and "{" in tpl:
             assert _sel([R.JSONValue(pattern=tpl)]) == [want], tpl
+    # placeholders with the reference's modifiers (json_test.go:165-169, :180-187): built
+    # text from the select path's text slots
+    mod_cases = [("Username: {auth.identity.username.@case:upper}", "Username: JOHN"),
+                 ('Domain: {auth.identity.email.@extract:{"sep":"@","pos":1}}', "Domain: test"),
+                 (r'Github username: {auth.identity.github\.com|@extract:{"sep":"/","pos":3}|@case:upper}',
+                  "Github username: JOHN"),
+                 (r'\{"msg":"I can build a JSON with dynamic values","username":"{auth.identity.github\.com|'
+                  r'@extract:{"sep":"/","pos":3}|@case:upper}"\}',
+                  '{"msg":"I can build a JSON with dynamic values","username":"JOHN"}')]
+    for tpl, want in mod_cases:
+        out = []
+        for kind, s in R.template_segments(tpl):
+            out.append(s if kind == "lit" else O.gjson_string_mods(DOC, s).decode())
+        assert "".join(out) == want, tpl
+        assert _sel([R.JSONValue(pattern=tpl)]) == [want], tpl
     segs = R.template_segments(r'\{"msg":"x","username":"{auth.identity.github\.com|@extract:{"sep":"/","pos":3}'
                                r'|@case:upper}"\}')
     assert segs == [("lit", '{"msg":"x","username":"'),
