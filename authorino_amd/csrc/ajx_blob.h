@@ -70,7 +70,10 @@ struct Selector {
 // :258-264), applied in order to the raw JSON of the selected value (a path such as
 // `auth.identity.email.@extract:{"sep":"@","pos":1}|@case:upper`). Evaluated by the
 // exact scan only (ajx_modifiers.h).
-enum : uint8_t { M_EXTRACT = 1, M_REPLACE = 2, M_CASE = 3, M_BASE64 = 4, M_STRIP = 5 };
+// M_FROMSTR is gjson's own @fromstr (v1.14.0 modFromStr: Parse(json).String() of a Valid
+// text); M_PATH is the path gjson Gets from a modifier's output (`@fromstr|a.b`,
+// a_off / a_len: its Components).
+enum : uint8_t { M_EXTRACT = 1, M_REPLACE = 2, M_CASE = 3, M_BASE64 = 4, M_STRIP = 5, M_FROMSTR = 6, M_PATH = 7 };
 struct Modifier {
     uint8_t kind;
     uint8_t variant;  // CASE 1 upper / 2 lower; BASE64 1 encode / 2 decode; 0: returns its input

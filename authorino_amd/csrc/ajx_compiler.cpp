@@ -262,7 +262,24 @@ int split_modifiers(const std::string& path, std::string* base, std::vector<ModS
     *base = path.substr(0, cut);
     size_t i = cut + 1;  // at '@'
     while (i < path.size()) {
-        if (path[i] != '@') return -1;  // a path component after a modifier
+        if (path[i] != '@') {
+            // a path after a modifier (`...|@fromstr|request.object.kind`): gjson Gets it
+            // from the modifier's output (Get: execModifier, then Get(rjson, path[1:])),
+            // up to the next '|@' / '.@'
+            size_t e = i;
+            for (; e < path.size(); e++) {
+                if (path[e] == '\\') { e++; continue; }
+                if ((path[e] == '|' || path[e] == '.') && e + 1 < path.size() && path[e + 1] == '@') break;
+            }
+            if (e > path.size()) e = path.size();
+            ModSpec m;
+            m.kind = M_PATH;
+            m.a = path.substr(i, e - i);
+            mods->push_back(m);
+            if (e >= path.size()) break;
+            i = e + 1;
+            continue;
+        }
         size_t k = i + 1;
         while (k < path.size() && path[k] != ':' && path[k] != '|' && path[k] != '.') k++;
         const std::string name = path.substr(i + 1, k - i - 1);
@@ -337,8 +354,10 @@ int split_modifiers(const std::string& path, std::string* base, std::vector<ModS
             m.variant = arg == "encode" ? 1 : arg == "decode" ? 2 : 0;
         } else if (name == "strip") {
             m.kind = M_STRIP;
+        } else if (name == "fromstr") {  // gjson v1.14.0 modFromStr
+            m.kind = M_FROMSTR;
         } else {
-            return -1;  // gjson's own modifiers (@this, @reverse, @fromstr, ...) are not compiled
+            return -1;  // gjson's other built-ins (@this, @reverse, @tostr, ...) are not compiled
         }
         mods->push_back(m);
         if (next >= path.size()) break;
@@ -551,10 +570,19 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             std::string base = sel;
             std::vector<ModSpec> mspec;
             const int mr = split_modifiers(sel, &base, &mspec);
-            const bool ok_path = mr >= 0 && split_selector(base, &pc);
+            bool ok_path = mr >= 0 && split_selector(base, &pc);
             bool counted = false;  // a '#' count or list: the exact scan (no modifier chain after it)
             for (const PathComponent& c : pc) counted = counted || c.array_index == kArrCount || c.array_index == kArrList;
-            if (!ok_path || (counted && !mspec.empty()) || comps.size() + pc.size() > 0xFFFFu ||
+            // the paths after modifiers: plain keys / indices (no '#', no modifier inside)
+            std::vector<std::vector<PathComponent>> tails(mspec.size());
+            size_t n_tail = 0;
+            for (size_t k = 0; k < mspec.size() && ok_path; k++) {
+                if (mspec[k].kind != M_PATH) continue;
+                ok_path = split_selector(mspec[k].a, &tails[k]) && !tails[k].empty();
+                for (const PathComponent& c : tails[k]) ok_path = ok_path && c.array_index != kArrCount && c.array_index != kArrList;
+                n_tail += tails[k].size();
+            }
+            if (!ok_path || (counted && !mspec.empty()) || comps.size() + pc.size() + n_tail > 0xFFFFu ||
                 mods.size() + mspec.size() > 0xFFFFu) {
                 p.state = P_UNSUPPORTED;
                 out->pattern_status[i] = AUTHJX_PAT_UNSUPPORTED;
@@ -567,11 +595,31 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             s.comp_count = (uint16_t)pc.size();
             s.mod_begin = (uint16_t)mods.size();
             s.mod_count = (uint16_t)mspec.size();
-            for (const ModSpec& m : mspec) {
+            auto push_comps = [&](const std::vector<PathComponent>& v) {
+                for (const PathComponent& c : v) {
+                    Component k;
+                    k.lit_off = (uint32_t)lits.size();
+                    k.lit_len = (uint32_t)c.key.size();
+                    k.array_index = c.array_index;
+                    k.hash = fnv1a(c.key);
+                    lits += c.key;
+                    comps.push_back(k);
+                }
+            };
+            push_comps(pc);  // (the selector's own components first: comp_begin)
+            for (size_t k = 0; k < mspec.size(); k++) {
+                const ModSpec& m = mspec[k];
                 Modifier r;
                 std::memset(&r, 0, sizeof r);
                 r.kind = m.kind;
                 r.variant = m.variant;
+                if (m.kind == M_PATH) {  // a_off / a_len: its components
+                    r.a_off = (uint32_t)comps.size();
+                    r.a_len = (uint32_t)tails[k].size();
+                    push_comps(tails[k]);
+                    mods.push_back(r);
+                    continue;
+                }
                 r.a_off = (uint32_t)lits.size();
                 r.a_len = (uint32_t)m.a.size();
                 lits += m.a;
@@ -580,15 +628,6 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 lits += m.b;
                 r.pos = m.pos;
                 mods.push_back(r);
-            }
-            for (const PathComponent& c : pc) {
-                Component k;
-                k.lit_off = (uint32_t)lits.size();
-                k.lit_len = (uint32_t)c.key.size();
-                k.array_index = c.array_index;
-                k.hash = fnv1a(c.key);
-                lits += c.key;
-                comps.push_back(k);
             }
             it = sel_ids.emplace(sel, (uint32_t)sels.size()).first;
             sels.push_back(s);

@@ -10,7 +10,11 @@
 // Zipf host traffic of config C4 repeats a few hosts), labels are read straight from the
 // host bytes from the last one up (no reversed copy of the key), and the tree's child maps
 // are looked up by string_view. Readers share a lock the writers (reconcile) take
-// exclusively, as the reference's RWMutex does (:51, :57, :68).
+// exclusively, as the reference's RWMutex does (:51, :57, :68) — writer-preferring like
+// Go's sync.RWMutex (a waiting Lock blocks new RLocks), so a constant lookup stream
+// cannot starve a reconcile.
+#include <pthread.h>
+
 #include <algorithm>
 #include <deque>
 #include <mutex>
@@ -49,11 +53,34 @@ struct RevLabels {
     }
 };
 
+// a reader / writer lock with writer preference (glibc's rwlock kind
+// PREFER_WRITER_NONRECURSIVE); the SharedMutex interface of std::shared_lock / unique_lock
+class RwLock {
+   public:
+    RwLock() {
+        pthread_rwlockattr_t a;
+        pthread_rwlockattr_init(&a);
+        pthread_rwlockattr_setkind_np(&a, PTHREAD_RWLOCK_PREFER_WRITER_NONRECURSIVE_NP);
+        pthread_rwlock_init(&l_, &a);
+        pthread_rwlockattr_destroy(&a);
+    }
+    ~RwLock() { pthread_rwlock_destroy(&l_); }
+    RwLock(const RwLock&) = delete;
+    RwLock& operator=(const RwLock&) = delete;
+    void lock() { pthread_rwlock_wrlock(&l_); }
+    void unlock() { pthread_rwlock_unlock(&l_); }
+    void lock_shared() { pthread_rwlock_rdlock(&l_); }
+    void unlock_shared() { pthread_rwlock_unlock(&l_); }
+
+   private:
+    pthread_rwlock_t l_;
+};
+
 }  // namespace
 
 struct authjx_index {
     std::deque<Node> nodes;  // (a deque: children's keys view labels that must not move)
-    mutable std::shared_mutex mu;
+    mutable RwLock mu;
     authjx_index() { nodes.emplace_back(); }  // the root, label "" (rootKeyLabel, index.go:13)
 
     // longestCommonLabel (index.go:205-223): the deepest node on the key's path and
@@ -160,7 +187,7 @@ void authjx_index_free(authjx_index* ix) { delete ix; }
 
 int authjx_index_set(authjx_index* ix, const char* key, uint32_t key_len, int32_t set_id, int override_) {
     if (!ix || (!key && key_len) || set_id < 0) return AUTHJX_EINVAL;
-    std::unique_lock<std::shared_mutex> g(ix->mu);
+    std::unique_lock<RwLock> g(ix->mu);
     try {
         return ix->set(std::string_view(key ? key : "", key_len), set_id, override_ != 0);
     } catch (...) {
@@ -170,14 +197,14 @@ int authjx_index_set(authjx_index* ix, const char* key, uint32_t key_len, int32_
 
 int authjx_index_delete_key(authjx_index* ix, const char* key, uint32_t key_len, int32_t set_id) {
     if (!ix || (!key && key_len)) return AUTHJX_EINVAL;
-    std::unique_lock<std::shared_mutex> g(ix->mu);
+    std::unique_lock<RwLock> g(ix->mu);
     ix->del(std::string_view(key ? key : "", key_len), set_id);
     return AUTHJX_OK;
 }
 
 int authjx_index_get(const authjx_index* ix, const char* host, uint32_t host_len, int32_t* out_set) {
     if (!ix || !out_set || (!host && host_len)) return AUTHJX_EINVAL;
-    std::shared_lock<std::shared_mutex> g(ix->mu);
+    std::shared_lock<RwLock> g(ix->mu);
     *out_set = lookup_host(ix, std::string_view(host ? host : "", host_len));
     return AUTHJX_OK;
 }
@@ -185,7 +212,7 @@ int authjx_index_get(const authjx_index* ix, const char* host, uint32_t host_len
 int authjx_index_lookup_batch(const authjx_index* ix, const uint8_t* hosts, const uint64_t* offs,
                               const uint32_t* lens, uint32_t n, int32_t* out_sets, uint32_t n_threads) {
     if (!ix || (n && (!hosts || !offs || !lens || !out_sets))) return AUTHJX_EINVAL;
-    std::shared_lock<std::shared_mutex> g(ix->mu);
+    std::shared_lock<RwLock> g(ix->mu);
     uint32_t nt = n_threads ? n_threads : std::max(1u, std::thread::hardware_concurrency());
     nt = std::min<uint32_t>(nt, std::max<uint32_t>(1u, n / 4096u));
     auto work = [&](uint32_t lo, uint32_t hi) {

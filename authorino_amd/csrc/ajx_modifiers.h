@@ -297,6 +297,130 @@ AJX_HD bool build_list(const uint8_t* blob, const Selector& sel, const uint8_t* 
     return true;
 }
 
+// gjson Valid (v1.14.0 validpayload / validany / validobject / validarray / validstring /
+// validnumber / validtrue...): one JSON value with surrounding ' ' '\t' '\n' '\r' and
+// nothing else; strings are not checked for UTF-8. Iterative, containers on a bit stack.
+// Returns false when undecided (nesting deeper than the stack), *ok the verdict.
+AJX_HD bool json_valid(const uint8_t* d, uint32_t n, bool* ok) {
+    constexpr uint32_t kDepth = 256;
+    uint64_t stk[kDepth / 64];  // bit: 1 object, 0 array
+    uint32_t depth = 0, i = 0;
+    *ok = false;
+    auto ws = [&]() {
+        while (i < n && (d[i] == ' ' || d[i] == '\t' || d[i] == '\n' || d[i] == '\r')) i++;
+    };
+    auto is_digit = [&](uint32_t k) { return k < n && d[k] >= '0' && d[k] <= '9'; };
+    auto hex = [](uint8_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); };
+    auto string = [&]() -> bool {  // at the opening quote
+        for (i++; i < n; i++) {
+            const uint8_t c = d[i];
+            if (c < ' ') return false;
+            if (c == '"') {
+                i++;
+                return true;
+            }
+            if (c == '\\') {
+                if (++i == n) return false;
+                const uint8_t e = d[i];
+                if (e == 'u') {
+                    for (int j = 0; j < 4; j++)
+                        if (++i >= n || !hex(d[i])) return false;
+                } else if (e != '"' && e != '\\' && e != '/' && e != 'b' && e != 'f' && e != 'n' && e != 'r' &&
+                           e != 't') {
+                    return false;
+                }
+            }
+        }
+        return false;
+    };
+    auto word = [&](const char* w, uint32_t len) {
+        for (uint32_t k = 0; k < len; k++)
+            if (i + k >= n || d[i + k] != (uint8_t)w[k]) return false;
+        i += len;
+        return true;
+    };
+    ws();
+    for (;;) {
+        // a value at i
+        if (i >= n) return true;
+        const uint8_t c = d[i];
+        if (c == '{' || c == '[') {  // (an empty one goes on after it, like a scalar)
+            i++;
+            ws();
+            if (i < n && d[i] == (c == '{' ? '}' : ']')) {
+                i++;
+            } else {
+                if (depth == kDepth) return false;
+                if (c == '{') stk[depth >> 6] |= 1ull << (depth & 63);
+                else stk[depth >> 6] &= ~(1ull << (depth & 63));
+                depth++;
+                if (c == '{') {  // a key, ':' and the member's value
+                    if (i >= n || d[i] != '"' || !string()) return true;
+                    ws();
+                    if (i >= n || d[i] != ':') return true;
+                    i++;
+                    ws();
+                }
+                continue;
+            }
+        } else if (c == '"') {
+            if (!string()) return true;
+        } else if (c == '-' || (c >= '0' && c <= '9')) {
+            if (c == '-') {
+                i++;
+                if (!is_digit(i)) return true;
+            }
+            if (d[i] == '0') i++;
+            else
+                while (is_digit(i)) i++;
+            if (i < n && d[i] == '.') {
+                i++;
+                if (!is_digit(i)) return true;
+                while (is_digit(i)) i++;
+            }
+            if (i < n && (d[i] == 'e' || d[i] == 'E')) {
+                i++;
+                if (i < n && (d[i] == '+' || d[i] == '-')) i++;
+                if (!is_digit(i)) return true;
+                while (is_digit(i)) i++;
+            }
+        } else if (c == 't') {
+            if (!word("true", 4)) return true;
+        } else if (c == 'f') {
+            if (!word("false", 5)) return true;
+        } else if (c == 'n') {
+            if (!word("null", 4)) return true;
+        } else {
+            return true;
+        }
+        // after a value: the container's ',' / closer, or the end of the text
+        for (;;) {
+            ws();
+            if (depth == 0) {
+                *ok = i == n;
+                return true;
+            }
+            const bool obj = (stk[(depth - 1) >> 6] >> ((depth - 1) & 63)) & 1u;
+            if (i >= n) return true;
+            if (d[i] == ',') {
+                i++;
+                ws();
+                if (obj) {
+                    if (i >= n || d[i] != '"' || !string()) return true;
+                    ws();
+                    if (i >= n || d[i] != ':') return true;
+                    i++;
+                    ws();
+                }
+                break;  // the next value
+            }
+            if (d[i] != (obj ? '}' : ']')) return true;
+            i++;
+            depth--;
+        }
+    }
+}
+
 // Run the selector's modifier chain on the value v of document doc: the final gjson
 // Result as (*rdoc, *rv). Returns false when undecided. A value that does not exist stays
 // Null (gjson pipes into the modifiers only from a found value).
@@ -409,6 +533,26 @@ AJX_HD bool apply_modifiers(const uint8_t* blob, const Selector& sel, const uint
                     if (c >= 0x80) return false;  // (unicode.IsPrint tables)
                     if (c >= 0x20 && c != 0x7F) o.put(c);
                 }
+                break;
+            }
+            case M_FROMSTR: {  // gjson modFromStr: "" unless Valid(json), else Parse(json).String()
+                bool ok;
+                if (!json_valid(in, in_n, &ok)) return false;
+                if (!ok) break;
+                if (!mod_result_string(in, in_n, outp, t)) return false;
+                o.put(mb.t, t.n);
+                break;
+            }
+            case M_PATH: {  // Get(previous output, path): its raw text; not found: Null
+                const Component* tc = (const Component*)(blob + h->off_components) + m.a_off;
+                const ValueRef v = gj_get(in, in_n, tc, m.a_len, lits);
+                if (v.esc == kValCount || v.esc == kValList) return false;  // (not compiled in tails)
+                if (v.end <= v.start) {
+                    *rdoc = in;
+                    *rv = ValueRef{0, 0, T_NULL, 0};
+                    return true;
+                }
+                o.put(in + v.start, v.end - v.start);
                 break;
             }
             default: return false;

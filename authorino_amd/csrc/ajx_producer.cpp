@@ -256,7 +256,8 @@ bool put_value(Tape& tp, std::string& o, int depth) {
                 size_t v0, v1;
             };
             std::vector<M> ms;
-            ms.reserve(cnt);
+            // (a member takes >= 5 tape bytes: a malformed count must not size the vector)
+            ms.reserve(std::min<size_t>(cnt, (tp.n - std::min(tp.i, tp.n)) / 5));
             for (uint32_t k = 0; k < cnt && tp.ok; k++) {
                 M m;
                 m.kl = tp.u32();

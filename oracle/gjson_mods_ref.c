@@ -9,7 +9,10 @@
  * the argument, and Parse of each output; plus Go's encoding/base64 Std / RawStd decoding
  * (partial output on a CorruptInputError) and strings.Split / ReplaceAll.
  * ToUpper / ToLower and unicode.IsPrint are restated for ASCII text; a non-ASCII text
- * there is reported undecided, as the device does.
+ * there is reported undecided, as the device does. gjson's own @fromstr (modFromStr:
+ * Parse(json).String() when Valid(json), else "") and a path after a modifier (Get:
+ * execModifier, then Get(rjson, path[1:])) are restated too, with gjson's recursive
+ * validator (validpayload, validany, validobject, validarray, validstring, validnumber).
  */
 #include <math.h>
 #include <stdlib.h>
@@ -153,7 +156,26 @@ int or_mod_split(const char* p, size_t n, size_t* base_len, or_mod* mods, int ma
     *base_len = cut;
     size_t i = cut + 1;
     while (i < n) {
-        if (p[i] != '@' || *n_mods >= max_mods) return -1;
+        if (*n_mods >= max_mods) return -1;
+        if (p[i] != '@') {  /* a path after a modifier, up to the next '|@' / '.@' */
+            size_t e = i;
+            while (e < n) {
+                if (p[e] == '\\') { e += 2; continue; }
+                if ((p[e] == '|' || p[e] == '.') && e + 1 < n && p[e + 1] == '@') break;
+                e++;
+            }
+            if (e > n) e = n;
+            or_mod* m = &mods[*n_mods];
+            memset(m, 0, sizeof *m);
+            (*n_mods)++;
+            m->kind = OR_MOD_PATH;
+            m->a = (char*)malloc(e - i + 1);
+            memcpy(m->a, p + i, e - i);
+            m->a_len = e - i;
+            if (e >= n) break;
+            i = e + 1;
+            continue;
+        }
         size_t k = i + 1;
         while (k < n && p[k] != ':' && p[k] != '|' && p[k] != '.') k++;
         const char* name = p + i + 1;
@@ -209,6 +231,8 @@ int or_mod_split(const char* p, size_t n, size_t* base_len, or_mod* mods, int ma
             m->variant = ARG_IS("encode") ? 1 : ARG_IS("decode") ? 2 : 0;
         } else if (NAME_IS("strip")) {
             m->kind = OR_MOD_STRIP;
+        } else if (NAME_IS("fromstr")) {
+            m->kind = OR_MOD_FROMSTR;
         } else {
             return -1;
         }
@@ -388,6 +412,133 @@ static void go_b64_encode(const unsigned char* s, size_t n, or_buf* out) {
     }
 }
 
+/* gjson v1.14.0 validator, recursive as gjson's: each returns the index after the value
+ * and sets *ok */
+static size_t v_any(const char* s, size_t n, size_t i, int* ok);
+static int v_ws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+static size_t v_string(const char* s, size_t n, size_t i, int* ok) { /* i after the quote */
+    for (; i < n; i++) {
+        unsigned char c = (unsigned char)s[i];
+        if (c < ' ') { *ok = 0; return i; }
+        if (c == '\\') {
+            if (++i == n) { *ok = 0; return i; }
+            switch (s[i]) {
+                case '"': case '\\': case '/': case 'b': case 'f': case 'n': case 'r': case 't': break;
+                case 'u':
+                    for (int j = 0; j < 4; j++) {
+                        i++;
+                        if (i >= n || !((s[i] >= '0' && s[i] <= '9') || (s[i] >= 'a' && s[i] <= 'f') ||
+                                        (s[i] >= 'A' && s[i] <= 'F'))) { *ok = 0; return i; }
+                    }
+                    break;
+                default: *ok = 0; return i;
+            }
+        } else if (c == '"') {
+            *ok = 1;
+            return i + 1;
+        }
+    }
+    *ok = 0;
+    return i;
+}
+static size_t v_number(const char* s, size_t n, size_t i, int* ok) { /* i after the first char */
+    i--;
+#define DIG(k) ((k) < n && s[k] >= '0' && s[k] <= '9')
+    *ok = 0;
+    if (s[i] == '-') { i++; if (!DIG(i)) return i; }
+    if (s[i] == '0') i++;
+    else while (DIG(i)) i++;
+    if (i < n && s[i] == '.') { i++; if (!DIG(i)) return i; while (DIG(i)) i++; }
+    if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+        i++;
+        if (i < n && (s[i] == '+' || s[i] == '-')) i++;
+        if (!DIG(i)) return i;
+        while (DIG(i)) i++;
+    }
+#undef DIG
+    *ok = 1;
+    return i;
+}
+static size_t v_comma(const char* s, size_t n, size_t i, char end, int* ok) {
+    for (; i < n; i++) {
+        if (v_ws(s[i])) continue;
+        *ok = s[i] == ',' || s[i] == end;
+        return i;
+    }
+    *ok = 0;
+    return i;
+}
+static size_t v_array(const char* s, size_t n, size_t i, int* ok) { /* after '[' */
+    for (; i < n; i++) {
+        if (v_ws(s[i])) continue;
+        if (s[i] == ']') { *ok = 1; return i + 1; }
+        for (;;) {
+            i = v_any(s, n, i, ok);
+            if (!*ok) return i;
+            i = v_comma(s, n, i, ']', ok);
+            if (!*ok) return i;
+            if (s[i] == ']') return i + 1;
+            i++;
+        }
+    }
+    *ok = 0;
+    return i;
+}
+static size_t v_object(const char* s, size_t n, size_t i, int* ok) { /* after '{' */
+    for (; i < n; i++) {
+        if (v_ws(s[i])) continue;
+        if (s[i] == '}') { *ok = 1; return i + 1; }
+        if (s[i] != '"') { *ok = 0; return i; }
+        for (;;) {  /* at a key's quote */
+            i = v_string(s, n, i + 1, ok);
+            if (!*ok) return i;
+            while (i < n && v_ws(s[i])) i++;
+            if (i >= n || s[i] != ':') { *ok = 0; return i; }
+            i = v_any(s, n, i + 1, ok);
+            if (!*ok) return i;
+            i = v_comma(s, n, i, '}', ok);
+            if (!*ok) return i;
+            if (s[i] == '}') return i + 1;
+            i++;
+            while (i < n && v_ws(s[i])) i++;
+            if (i >= n || s[i] != '"') { *ok = 0; return i; }
+        }
+    }
+    *ok = 0;
+    return i;
+}
+static size_t v_word(const char* s, size_t n, size_t i, const char* rest, int* ok) {
+    size_t L = strlen(rest);
+    *ok = i + L <= n && !memcmp(s + i, rest, L);
+    return *ok ? i + L : i;
+}
+static size_t v_any(const char* s, size_t n, size_t i, int* ok) {
+    for (; i < n; i++) {
+        switch (s[i]) {
+            case ' ': case '\t': case '\n': case '\r': continue;
+            case '{': return v_object(s, n, i + 1, ok);
+            case '[': return v_array(s, n, i + 1, ok);
+            case '"': return v_string(s, n, i + 1, ok);
+            case '-': case '0': case '1': case '2': case '3': case '4': case '5': case '6': case '7': case '8':
+            case '9': return v_number(s, n, i + 1, ok);
+            case 't': return v_word(s, n, i + 1, "rue", ok);
+            case 'f': return v_word(s, n, i + 1, "alse", ok);
+            case 'n': return v_word(s, n, i + 1, "ull", ok);
+            default: *ok = 0; return i;
+        }
+    }
+    *ok = 0;
+    return i;
+}
+int or_valid(const char* s, size_t n) {
+    int ok = 0;
+    size_t i = v_any(s, n, 0, &ok);
+    if (!ok) return 0;
+    for (; i < n; i++)
+        if (!v_ws(s[i])) return 0;
+    return 1;
+}
+
 static void wrap_into(const char* s, size_t n, or_buf* out) {
     or_buf_push(out, "\"", 1);
     or_buf_push(out, s, n);
@@ -493,12 +644,32 @@ int or_mod_apply(const or_mod* mods, int n_mods, const char* raw, size_t raw_len
                 }
                 break;
             }
+            case OR_MOD_FROMSTR: {
+                if (!or_valid(in, in_n)) break; /* "" */
+                if (parse_string_of(in, in_n, &nxt) != 0) rc = -1;
+                break;
+            }
+            case OR_MOD_PATH: {
+                or_result r;
+                memset(&r, 0, sizeof r);
+                if (or_gjson_get(in, in_n, m->a, m->a_len, &r) != 0) { rc = -1; or_result_free(&r); break; }
+                if (r.raw_len == 0) { /* not found: the Result is Null, the chain ends */
+                    or_result_free(&r);
+                    or_buf_reset(&cur);
+                    k = n_mods;
+                    goto done;
+                }
+                or_buf_push(&nxt, r.raw, r.raw_len);
+                or_result_free(&r);
+                break;
+            }
             default: rc = -1;
         }
         or_buf t = cur;
         cur = nxt;
         nxt = t;
     }
+done:
     if (rc == 0) {
         or_buf_reset(text);
         or_buf_push(text, cur.p ? cur.p : "", cur.n);

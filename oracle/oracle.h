@@ -73,7 +73,10 @@ void or_result_string(const or_result* r, or_buf* out);
 int or_result_array_next(const or_result* r, size_t* cursor, or_result* item);
 
 /* ---- the reference's gjson modifiers (pkg/json/json.go:161-264; gjson_mods_ref.c) ---- */
-enum { OR_MOD_EXTRACT = 1, OR_MOD_REPLACE = 2, OR_MOD_CASE = 3, OR_MOD_BASE64 = 4, OR_MOD_STRIP = 5 };
+enum { OR_MOD_EXTRACT = 1, OR_MOD_REPLACE = 2, OR_MOD_CASE = 3, OR_MOD_BASE64 = 4, OR_MOD_STRIP = 5,
+       OR_MOD_FROMSTR = 6 /* gjson's own @fromstr */, OR_MOD_PATH = 7 /* a path Get after a modifier (a) */ };
+/* gjson Valid (validpayload): 1 when s[0..n) is one JSON value with surrounding whitespace */
+int or_valid(const char* s, size_t n);
 typedef struct {
     int kind, variant, has_old;
     char* a; /* extract: sep; replace: old */

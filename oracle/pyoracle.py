@@ -67,6 +67,8 @@ def lib():
         L.or_gjson_get_mods.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(_Result),
                                         C.POINTER(_Buf)]
         L.or_gjson_get_mods.restype = C.c_int
+        L.or_valid.argtypes = [C.c_char_p, C.c_size_t]
+        L.or_valid.restype = C.c_int
         L.or_result_string.argtypes = [C.POINTER(_Result), C.POINTER(_Buf)]
         L.or_result_array_next.argtypes = [C.POINTER(_Result), C.POINTER(C.c_size_t), C.POINTER(_Result)]
         L.or_result_array_next.restype = C.c_int
@@ -142,6 +144,12 @@ def gjson_string_mods(doc, path):
     L.or_result_free(C.byref(r))
     L.or_buf_free(C.byref(text))
     return out
+
+
+def valid(text) -> bool:
+    """gjson Valid (or_valid, the recursive restatement)."""
+    d = _b(text)
+    return lib().or_valid(d, len(d)) == 1
 
 
 def gjson_get_mods(doc, path):

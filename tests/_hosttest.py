@@ -41,6 +41,8 @@ def lib():
         L.ht_select_value.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ht_select_value.restype = C.c_int
+        L.ht_json_valid.argtypes = [C.c_char_p, C.c_uint32]
+        L.ht_json_valid.restype = C.c_int
         L.ht_string.restype = C.c_int
         L.ht_regex.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
         L.ht_regex.restype = C.c_void_p
@@ -224,3 +226,9 @@ def lean_last_dec():
     out = (C.c_uint64 * 2)()
     L.ht_lean_last_dec(out)
     return out[0], out[1]
+
+
+def json_valid(text) -> int:
+    """gjson Valid as the device restates it: 1 / 0, -1 undecided (nesting > 256)."""
+    d = _b(text)
+    return lib().ht_json_valid(d, len(d))

@@ -92,6 +92,13 @@ int ht_select_value(void* h, uint32_t p, const uint8_t* doc_in, uint32_t len, ui
     return select_value(blob, sels[pats[p].selector], doc, len, mb, text, cap, used, out) ? 0 : -1;
 }
 
+// json_valid (ajx_modifiers.h, gjson Valid): 1 valid, 0 invalid, -1 undecided (depth)
+int ht_json_valid(const uint8_t* d, uint32_t n) {
+    bool ok;
+    if (!json_valid(d, n, &ok)) return -1;
+    return ok ? 1 : 0;
+}
+
 // value resolution only: type + raw span
 int ht_get(const char* path, uint32_t plen, const uint8_t* doc_in, uint32_t len, uint32_t* start, uint32_t* end) {
     std::vector<uint8_t> buf(len + 32, 0);

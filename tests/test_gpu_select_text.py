@@ -167,3 +167,48 @@ def test_denywith_and_cache_keys_with_modifiers_on_device(ctx):
     c = cache_cfg()
     res = P.AuthPipelineBatch(P.AuthConfig(authorization=[c]), ctx=ctx).evaluate([_req(tenant="ACME")])
     assert res[0].code == P.CODE_OK and c.cache.get("acme/alice") is True
+
+
+def test_fromstr_and_tails_on_device(ctx):
+    """gjson's @fromstr and a path after a modifier (validating-webhook.md:156,
+    json_test.go:247-257) through the kernels: selected values (type + raw) and pattern
+    results (eq / neq / incl against values from the documents, T bitmap and tri-state)
+    equal the oracle's on AdmissionReview-shaped, malformed and scalar bodies."""
+    from authorino_amd import runtime
+    from test_fromstr import PATHS, _fromstr_doc, _jwt_doc
+
+    rng = random.Random(99)
+    docs = [_fromstr_doc(rng) for _ in range(3000)] + [_jwt_doc()]
+    arena, offs, lens = _pack(docs)
+    rs = ctx.compile([(p, 1, "") for p in PATHS], [], -1)
+    assert rs.status == [0] * len(PATHS)
+    vals, text = ctx.select_text_host_arena([rs], arena, offs, lens, text_stride=8192)
+    checked = und = 0
+    for k, d in enumerate(docs):
+        for j, p in enumerate(PATHS):
+            want = O.gjson_get_mods(d, p)
+            if (int(vals[k, j, 2]) & 0xFF) == 255:
+                und += 1
+                continue
+            assert want is not None, (d, p)
+            _check(vals, text, k, j, d, want)
+            checked += 1
+    assert checked > 25000 and und <= checked // 20, (checked, und)
+    jwt = 'access_token.@extract:{"pos":1}|@extract:{"sep":".","pos":1}|@base64:decode|@fromstr'
+    pats = [(PATHS[1], 1, "authorino"), (PATHS[1], 2, "authorino"), (PATHS[3], 1, "AdmissionReview"),
+            (PATHS[2], 3, "AdmissionReview"), (PATHS[0], 1, ""), (PATHS[7], 1, "5"), (PATHS[9], 1, "v"),
+            (PATHS[4], 1, "DEFAULT"), (jwt + ".exp", 1, "1685557675"), (jwt + ".aud", 3,
+                                                                          "https://kubernetes.default.svc.cluster.local")]
+    nodes = [(0, -1, -1, i) for i in range(len(pats))]
+    root = -1
+    for i in reversed(range(len(pats))):
+        nodes.append((2, i, root, -1))  # (an Or chain: every pattern is evaluated)
+        root = len(nodes) - 1
+    dev = ctx.compile(pats, nodes, root)
+    orc = O.Ruleset(pats, nodes, root)
+    tri, _, bm = ctx.eval_host_arena([dev], arena, offs, lens)
+    otri, _, obm = O.eval_batch([orc], arena, offs, lens, nthreads=8)
+    ok = tri != runtime.UNDECIDED
+    assert ok.sum() >= 0.95 * len(docs)
+    assert np.array_equal(tri[ok], otri[ok]) and np.array_equal(bm[ok], obm[ok])
+    assert (bm[-1, 0] >> 8) & 1 and (bm[-1, 0] >> 9) & 1  # (the JWT claims)
