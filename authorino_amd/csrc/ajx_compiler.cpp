@@ -256,7 +256,8 @@ int split_modifiers(const std::string& path, std::string* base, std::vector<ModS
     size_t cut = std::string::npos;
     for (size_t i = 0; i + 1 < path.size(); i++) {
         if (path[i] == '\\') { i++; continue; }
-        if ((path[i] == '.' || path[i] == '|') && path[i + 1] == '@') { cut = i; break; }
+        // a modifier, or a pipe: `a|b` is Get(Get(json, a).Raw, b) (a path after the cut)
+        if (((path[i] == '.' || path[i] == '|') && path[i + 1] == '@') || path[i] == '|') { cut = i; break; }
     }
     if (cut == std::string::npos || cut == 0) return 0;
     *base = path.substr(0, cut);
@@ -269,7 +270,7 @@ int split_modifiers(const std::string& path, std::string* base, std::vector<ModS
             size_t e = i;
             for (; e < path.size(); e++) {
                 if (path[e] == '\\') { e++; continue; }
-                if ((path[e] == '|' || path[e] == '.') && e + 1 < path.size() && path[e + 1] == '@') break;
+                if (path[e] == '|' || (path[e] == '.' && e + 1 < path.size() && path[e + 1] == '@')) break;
             }
             if (e > path.size()) e = path.size();
             ModSpec m;

@@ -150,7 +150,7 @@ int or_mod_split(const char* p, size_t n, size_t* base_len, or_mod* mods, int ma
     int found = 0;
     for (size_t i = 0; i + 1 < n; i++) {
         if (p[i] == '\\') { i++; continue; }
-        if ((p[i] == '.' || p[i] == '|') && p[i + 1] == '@') { cut = i; found = 1; break; }
+        if (p[i] == '|' || (p[i] == '.' && p[i + 1] == '@')) { cut = i; found = 1; break; }
     }
     if (!found || cut == 0) return 0;
     *base_len = cut;
@@ -161,7 +161,7 @@ int or_mod_split(const char* p, size_t n, size_t* base_len, or_mod* mods, int ma
             size_t e = i;
             while (e < n) {
                 if (p[e] == '\\') { e += 2; continue; }
-                if ((p[e] == '|' || p[e] == '.') && e + 1 < n && p[e + 1] == '@') break;
+                if (p[e] == '|' || (p[e] == '.' && e + 1 < n && p[e + 1] == '@')) break;
                 e++;
             }
             if (e > n) e = n;
