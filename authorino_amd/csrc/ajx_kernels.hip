@@ -852,6 +852,9 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
         }
     } else if (mode != 40 && !(d_set_of_req && !shared)) {  // the lean single-pass kernel (default)
+        // (multi-tenant batches: the staged tenant scanner below. Measured on c4, the lean
+        // scan with per-lane table parameters took 6.39 ms and one pass per ruleset of a
+        // wave 7.3-7.8 ms, against 5.38 ms for the tenant kernel's LDS-staged tables)
         const uint32_t lblock = shared ? lean_block(shared_blob_bytes) : 256u;
         const uint32_t lgrid = (n + lblock - 1) / lblock;
         const uint32_t llds = ring_off + (lblock / 64) * kLeanRingBytesPerWave;

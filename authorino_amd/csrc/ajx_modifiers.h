@@ -7,16 +7,19 @@
 //
 //   extract  Parse(json).String() split on sep; part pos wrapped in quotes, "n" past the end
 //   replace  Parse(json).String() with every old -> new, wrapped (no argument: unchanged)
-//   case     strings.ToUpper / ToLower of the raw text (upper / lower; else unchanged)
+//   case     strings.ToUpper / ToLower of the raw text (upper / lower; else unchanged),
+//            Unicode simple mappings from ajx_unicode.h
 //   base64   encode: StdEncoding of Parse(json).String(), wrapped; decode: StdEncoding when
 //            the length is a multiple of 4 and it decodes, else RawStdEncoding's partial
 //            result; quotes escaped, wrapped (else unchanged)
-//   strip    the runes unicode.IsPrint keeps, of the raw text
-// Unicode case mapping and IsPrint beyond ASCII, texts over kModBuf bytes and Parse of a
+//   strip    the runes unicode.IsPrint keeps, of the raw text (ajx_unicode.h)
+// Code points ajx_unicode.h cannot vouch for (unassigned in its Unicode version, special
+// casing), texts over kModBuf bytes and Parse of a
 // text starting with an uncommon number character ('+' 'i' 'I' 'N', "n" not "null") are
 // left undecided (the request's pattern is AUTHJX_UNDECIDED).
 #pragma once
 #include "ajx_device.h"
+#include "ajx_unicode.h"
 
 namespace ajx {
 
@@ -297,6 +300,74 @@ AJX_HD bool build_list(const uint8_t* blob, const Selector& sel, const uint8_t* 
     return true;
 }
 
+// Go's utf8.DecodeRune of s[i..n): the rune and its width; an invalid or truncated
+// sequence (overlong, surrogate, > U+10FFFF) is U+FFFD of width 1, as `range` over a
+// string yields it
+AJX_HD uint32_t go_decode_rune(const uint8_t* s, uint32_t n, uint32_t i, uint32_t* w) {
+    const uint32_t b0 = s[i];
+    *w = 1;
+    if (b0 < 0x80) return b0;
+    auto cont = [&](uint32_t k, uint32_t lo, uint32_t hi) { return i + k < n && s[i + k] >= lo && s[i + k] <= hi; };
+    if (b0 >= 0xC2 && b0 <= 0xDF) {
+        if (!cont(1, 0x80, 0xBF)) return 0xFFFD;
+        *w = 2;
+        return ((b0 & 0x1F) << 6) | (s[i + 1] & 0x3F);
+    }
+    if (b0 >= 0xE0 && b0 <= 0xEF) {
+        const uint32_t lo = b0 == 0xE0 ? 0xA0 : 0x80, hi = b0 == 0xED ? 0x9F : 0xBF;
+        if (!cont(1, lo, hi) || !cont(2, 0x80, 0xBF)) return 0xFFFD;
+        *w = 3;
+        return ((b0 & 0x0F) << 12) | ((s[i + 1] & 0x3Fu) << 6) | (s[i + 2] & 0x3F);
+    }
+    if (b0 >= 0xF0 && b0 <= 0xF4) {
+        const uint32_t lo = b0 == 0xF0 ? 0x90 : 0x80, hi = b0 == 0xF4 ? 0x8F : 0xBF;
+        if (!cont(1, lo, hi) || !cont(2, 0x80, 0xBF) || !cont(3, 0x80, 0xBF)) return 0xFFFD;
+        *w = 4;
+        return ((b0 & 0x07) << 18) | ((s[i + 1] & 0x3Fu) << 12) | ((s[i + 2] & 0x3Fu) << 6) | (s[i + 3] & 0x3F);
+    }
+    return 0xFFFD;
+}
+
+// utf8.EncodeRune (the runes here are valid)
+AJX_HD void put_rune(OutBuf& o, uint32_t r) {
+    if (r < 0x80) {
+        o.put(r);
+    } else if (r < 0x800) {
+        o.put(0xC0 | (r >> 6));
+        o.put(0x80 | (r & 0x3F));
+    } else if (r < 0x10000) {
+        o.put(0xE0 | (r >> 12));
+        o.put(0x80 | ((r >> 6) & 0x3F));
+        o.put(0x80 | (r & 0x3F));
+    } else {
+        o.put(0xF0 | (r >> 18));
+        o.put(0x80 | ((r >> 12) & 0x3F));
+        o.put(0x80 | ((r >> 6) & 0x3F));
+        o.put(0x80 | (r & 0x3F));
+    }
+}
+
+// ajx_unicode.h tables: is r inside one of n sorted (lo, hi) ranges; r's mapping in n
+// sorted (code point, mapping) pairs (r itself when absent)
+AJX_HD bool uni_in_ranges(const uint32_t* t, uint32_t n, uint32_t r) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (t[2 * mid + 1] < r) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < n && t[2 * lo] <= r;
+}
+AJX_HD uint32_t uni_map(const uint32_t* t, uint32_t n, uint32_t r) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (t[2 * mid] < r) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < n && t[2 * lo] == r ? t[2 * lo + 1] : r;
+}
+
 // gjson Valid (v1.14.0 validpayload / validany / validobject / validarray / validstring /
 // validnumber / validtrue...): one JSON value with surrounding ' ' '\t' '\n' '\r' and
 // nothing else; strings are not checked for UTF-8. Iterative, containers on a bit stack.
@@ -490,13 +561,21 @@ AJX_HD bool apply_modifiers(const uint8_t* blob, const Selector& sel, const uint
                 o.put('"');
                 break;
             }
-            case M_CASE: {
-                for (uint32_t i = 0; i < in_n; i++) {
+            case M_CASE: {  // strings.ToUpper / ToLower: Map(unicode.ToUpper / ToLower)
+                for (uint32_t i = 0; i < in_n;) {
                     uint8_t c = in[i];
-                    if (c >= 0x80 && m.variant) return false;  // (Unicode case tables)
-                    if (m.variant == 1 && c >= 'a' && c <= 'z') c = (uint8_t)(c - 32);
-                    if (m.variant == 2 && c >= 'A' && c <= 'Z') c = (uint8_t)(c + 32);
-                    o.put(c);
+                    if (c < 0x80 || !m.variant) {
+                        if (m.variant == 1 && c >= 'a' && c <= 'z') c = (uint8_t)(c - 32);
+                        if (m.variant == 2 && c >= 'A' && c <= 'Z') c = (uint8_t)(c + 32);
+                        o.put(c);
+                        i++;
+                        continue;
+                    }
+                    uint32_t w;
+                    const uint32_t r = go_decode_rune(in, in_n, i, &w);  // (invalid: U+FFFD)
+                    i += w;
+                    if (uni_in_ranges(kUniUndecided, kUniUndecided_n, r)) return false;
+                    put_rune(o, m.variant == 1 ? uni_map(kUniUpper, kUniUpper_n, r) : uni_map(kUniLower, kUniLower_n, r));
                 }
                 break;
             }
@@ -527,11 +606,19 @@ AJX_HD bool apply_modifiers(const uint8_t* blob, const Selector& sel, const uint
                 o.n = w.n;
                 break;
             }
-            case M_STRIP: {
-                for (uint32_t i = 0; i < in_n; i++) {
+            case M_STRIP: {  // strings.Map dropping the runes unicode.IsPrint rejects
+                for (uint32_t i = 0; i < in_n;) {
                     const uint8_t c = in[i];
-                    if (c >= 0x80) return false;  // (unicode.IsPrint tables)
-                    if (c >= 0x20 && c != 0x7F) o.put(c);
+                    if (c < 0x80) {
+                        if (c >= 0x20 && c != 0x7F) o.put(c);
+                        i++;
+                        continue;
+                    }
+                    uint32_t w;
+                    const uint32_t r = go_decode_rune(in, in_n, i, &w);
+                    i += w;
+                    if (uni_in_ranges(kUniUndecided, kUniUndecided_n, r)) return false;
+                    if (uni_in_ranges(kUniPrint, kUniPrint_n, r)) put_rune(o, r);
                 }
                 break;
             }

@@ -1,0 +1,129 @@
+"""@case / @strip on non-ASCII text (pkg/json/json.go:208-216 strings.ToUpper / ToLower,
+:239-248 strings.Map with unicode.IsPrint) on the device's exact path (ajx_modifiers.h
+with the generated ajx_unicode.h, host build) against an independent restatement here:
+Go's `range` decoding (invalid / truncated / overlong / surrogate sequences are U+FFFD,
+width 1) via Python's strict UTF-8 decoder, the simple case mapping from str.upper() /
+str.lower() where it is one character, IsPrint as str.isprintable() (L M N P S and the
+ASCII space). Code points unassigned in this Python's Unicode (13.0; Go 1.21 has 15.0)
+and SpecialCasing characters must come back UNDECIDED, never guessed."""
+import json
+import random
+import unicodedata
+
+import pytest
+
+import _hosttest as H
+
+
+def _runes(b: bytes):
+    i = 0
+    while i < len(b):
+        if b[i] < 0x80:
+            yield chr(b[i]), b[i:i + 1]
+            i += 1
+            continue
+        for k in (2, 3, 4):
+            try:
+                c = b[i:i + k].decode("utf-8")
+            except UnicodeDecodeError:
+                continue
+            if len(c) == 1:
+                yield c, None
+                i += k
+                break
+        else:
+            yield "�", None
+            i += 1
+
+
+class Undecided(Exception):
+    pass
+
+
+def _vouch(c):
+    if ord(c) >= 0x80 and (unicodedata.category(c) == "Cn" or len(c.upper()) != 1 or len(c.lower()) != 1):
+        raise Undecided()
+
+
+def go_case(raw: bytes, upper: bool) -> bytes:
+    if all(x < 0x80 for x in raw):
+        return raw.upper() if upper else raw.lower()
+    out = []
+    for c, _ in _runes(raw):
+        _vouch(c)
+        out.append(c.upper() if upper else c.lower())
+    return "".join(out).encode("utf-8", "surrogatepass")
+
+
+def go_strip(raw: bytes) -> bytes:
+    out = []
+    for c, _ in _runes(raw):
+        if ord(c) >= 0x80:
+            _vouch(c)
+        if c.isprintable():
+            out.append(c)
+    return "".join(out).encode("utf-8")
+
+
+ALPH = ("aZé ßſİıǅΣσςΐДжԱաႠⴀᏸ𐐀𐐨ꭰﬀŉͅ ­​﻿\U0010fffd€漢😀͸ࣿ"
+        " \U0001e900\U0001e922ꞔᲐა")
+
+
+def _raw_string(rng):
+    parts = []
+    for _ in range(rng.randrange(0, 12)):
+        r = rng.random()
+        if r < 0.75:
+            parts.append(rng.choice(ALPH).encode("utf-8"))
+        elif r < 0.85:
+            parts.append(rng.choice([b"\xff", b"\xc3", b"\xe2\x82", b"\xed\xa0\x80", b"\xc0\xaf", b"\xf4\x90\x80\x80"]))
+        else:
+            parts.append(rng.choice([b"\\n", b"\\u00e9", b"\x01", b"\x7f", b"\\\""]))
+    return b'"' + b"".join(parts) + b'"'
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_case_and_strip_on_unicode_match_go(seed):
+    rng = random.Random(6100 + seed)
+    paths = {"s.@case:upper": lambda r: go_case(r, True), "s|@case:lower": lambda r: go_case(r, False),
+             "s.@strip": go_strip}
+    hrs = {p: H.HostRuleset([(p, 1, "")], [(0, -1, -1, 0)], 0) for p in paths}
+    decided = undecided = 0
+    for _ in range(1500):
+        raw = _raw_string(rng)
+        d = b'{"s":' + raw + b',"n":1}'
+        for p, f in paths.items():
+            try:
+                want = f(raw)
+            except Undecided:
+                want = None
+            rc, out, _ = hrs[p].select_value(0, d, text := bytearray(4096), 0)
+            if want is None:
+                assert rc == -1, (p, raw)
+                undecided += 1
+                continue
+            assert rc == 0, (p, raw)
+            st, ln, tt = out
+            src = bytes(text) if (tt >> 8) & 4 else d
+            got = src[st:st + ln]
+            # (the Result of Parse(output): the string token, up to its closing quote)
+            assert got == want[:len(got)] and len(got) >= min(len(want), 2), (p, raw, got, want)
+            decided += 1
+    assert decided > 2000 and undecided > 50, (decided, undecided)
+
+
+def test_unicode_kats():
+    """Go's behaviour on a few known cases (strings.ToUpper / ToLower / IsPrint)."""
+    cases = [("s.@case:upper", "é ſ ı ǆ", "É S I Ǆ"), ("s.@case:lower", "ÉKKΣ", "ékkσ"),
+             ("s.@case:upper", "straße", None), ("s.@case:lower", "İ", None),  # (SpecialCasing)
+             ("s.@strip", "a\u00a0b\u00adc\u200bd", "abcd"), ("s.@strip", "x€漢😀", "x€漢😀")]
+    for path, text, want in cases:
+        d = json.dumps({"s": text}, ensure_ascii=False).encode()
+        hr = H.HostRuleset([(path, 1, "")], [(0, -1, -1, 0)], 0)
+        rc, out, _ = hr.select_value(0, d, text_buf := bytearray(512), 0)
+        if want is None:
+            assert rc == -1, (path, text)
+            continue
+        assert rc == 0, (path, text)
+        got = bytes(text_buf[out[0]:out[0] + out[1]]).decode()
+        assert got == '"%s"' % want, (path, text, got)
