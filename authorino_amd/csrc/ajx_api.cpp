@@ -80,6 +80,7 @@ struct authjx_ctx {
     std::mutex batch_mu;           // serialises the host-buffer entry points (staging buffer)
     std::vector<Workspace*> ws;
     Workspace* last_ws = nullptr;  // of the last device call (last_kernel_ms / last_exact_count)
+    std::vector<authjx_batcher*> batchers;  // alive on this context (shutdown destroys them first)
     // staging for the host-buffer entry points
     uint8_t* d_stage = nullptr;
     size_t stage_cap = 0;
@@ -271,6 +272,14 @@ int authjx_init(int device, authjx_ctx** out) {
 
 void authjx_shutdown(authjx_ctx* ctx) {
     if (!ctx) return;
+    // batchers still alive: closed (their queued requests evaluated, workers joined) before
+    // the workspaces they use go away
+    std::vector<authjx_batcher*> live;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        live = ctx->batchers;
+    }
+    for (authjx_batcher* b : live) authjx_batcher_destroy(b);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (Workspace* w : ctx->ws) destroy_workspace(w);
@@ -798,12 +807,21 @@ int authjx_batcher_create(authjx_ctx* ctx, uint32_t max_batch, uint32_t window_u
     b->core = new ajx::BatchCore(
         max_batch, (uint64_t)window_us * 1000ull, queue_cap ? queue_cap : 4 * max_batch,
         [b](std::vector<ajx::BatchReq*>& reqs, uint32_t wid) { return b->evaluate(reqs, wid); }, kBatcherWorkers);
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        ctx->batchers.push_back(b);
+    }
     *out = b;
     return AUTHJX_OK;
 }
 
 void authjx_batcher_destroy(authjx_batcher* b) {
     if (!b) return;
+    {
+        std::lock_guard<std::mutex> g(b->ctx->mu);
+        auto& v = b->ctx->batchers;
+        v.erase(std::remove(v.begin(), v.end(), b), v.end());
+    }
     delete b->core;  // evaluates what is queued, joins the workers
     (void)hipSetDevice(b->ctx->device);
     for (auto& L : b->lanes) {

@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import threading
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -195,6 +196,7 @@ class Context:
         _check(L.authjx_init(device, C.byref(h)), "authjx_init")
         self._h = h
         self.device = device
+        self._batchers = weakref.WeakSet()  # (authjx_shutdown destroys those still alive)
 
     def compile(self, patterns: Sequence[Tuple[str, int, str]], nodes: Sequence[Tuple[int, int, int, int]],
                 root: int) -> "Ruleset":
@@ -369,6 +371,8 @@ class Context:
 
     def close(self):
         if getattr(self, "_h", None):
+            for b in list(getattr(self, "_batchers", ())):
+                b._h = None  # (destroyed by authjx_shutdown below)
             load_library().authjx_shutdown(self._h)
             self._h = None
 
@@ -497,6 +501,7 @@ class Batcher:
         _check(L.authjx_batcher_create(ctx._h, max_batch, window_us, queue_cap, C.byref(h)), "authjx_batcher_create")
         self.ctx = ctx
         self._h = h
+        ctx._batchers.add(self)
 
     def eval(self, ruleset: "Ruleset", doc, timeout_s: float = 0.0):
         """(tri-states, error indices) of `ruleset`'s trees on one document."""

@@ -125,7 +125,9 @@ typedef struct {
     int32_t root;
 } authjx_tree;
 
-/* Device context: one per GPU (device ordinal). */
+/* Device context: one per GPU (device ordinal). authjx_shutdown first destroys every
+ * micro-batcher still alive on the context (authjx_batcher_destroy: queued requests are
+ * evaluated); their handles are invalid afterwards. */
 int authjx_init(int device, authjx_ctx** out);
 void authjx_shutdown(authjx_ctx* ctx);
 // The sha256 (first 32 hex digits) of the sources the library was built from

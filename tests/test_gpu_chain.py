@@ -82,3 +82,18 @@ def test_native_index_selects_c4_rulesets_on_device(ctx):
     otri, oerr, obm = O.eval_batch(osets, w.arena, w.offs, w.lens, set_of_req=sor.astype(np.uint32), nthreads=8)
     assert (tri == 3).sum() == 0
     assert np.array_equal(tri, otri) and np.array_equal(err, oerr) and np.array_equal(bm, obm)
+
+
+def test_shutdown_destroys_live_batchers():
+    """authjx_shutdown with a micro-batcher still alive on the context: the
+    batcher is destroyed first (its queue drained, workers joined), no use after free."""
+    from authorino_amd import runtime
+
+    ctx = runtime.Context(0)
+    rs = ctx.compile([("a", 1, "x")], [(0, -1, -1, 0)], 0)
+    b = runtime.Batcher(ctx, max_batch=64, window_us=100)
+    tri, _ = b.eval(rs, b'{"a":"x"}')
+    assert int(tri[0]) == runtime.T
+    ctx.close()
+    assert b._h is None
+    b.close()  # (a no-op now)
