@@ -22,3 +22,4 @@ import sys, json
 for l in sys.stdin:
     d = json.loads(l); print(d['config'].get('workload'), round(d['ms_per_step'],3), round(d['roofline']['kernel_ms'],3), round(d['roofline']['frac'],4), d['roofline'].get('traffic'), d.get('parity'), d.get('exact_path_requests'), d.get('undecided'), (d.get('cpu_baseline') or {}).get('value'))"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo smoke ok || echo smoke failed
+cp pmc_traffic.json $O/pmc_traffic.json
