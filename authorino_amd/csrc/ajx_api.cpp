@@ -212,15 +212,22 @@ int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
     return AUTHJX_OK;
 }
 
-// a device call's workspace, locked: ctx->mu only while the workspace is looked up
+// a device call's workspace, locked: ctx->mu only while the workspace is looked up, not
+// while waiting for a busy stream's workspace (calls on the context's other streams, the
+// batcher's workers among them, go on meanwhile). A workspace lives until shutdown, or
+// until authjx_batcher_destroy for a batcher's private streams, which only its joined
+// workers used. Lock order: w->mu before ctx->mu.
 struct WsLock {
     Workspace* w = nullptr;
     std::unique_lock<std::mutex> lock;
     WsLock(authjx_ctx* ctx, void* stream) {
-        std::lock_guard<std::mutex> g(ctx->mu);
-        w = workspace_of(ctx, stream ? (hipStream_t)stream : ctx->stream);
+        {
+            std::lock_guard<std::mutex> g(ctx->mu);
+            w = workspace_of(ctx, stream ? (hipStream_t)stream : ctx->stream);
+        }
         if (w) {
             lock = std::unique_lock<std::mutex>(w->mu);
+            std::lock_guard<std::mutex> g(ctx->mu);
             ctx->last_ws = w;
         }
     }
