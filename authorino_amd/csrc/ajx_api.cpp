@@ -295,6 +295,28 @@ void authjx_shutdown(authjx_ctx* ctx) {
     delete ctx;
 }
 
+int authjx_release_stream(authjx_ctx* ctx, void* stream) {
+    if (!ctx || !stream || (hipStream_t)stream == ctx->stream) return AUTHJX_EINVAL;
+    Workspace* w = nullptr;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        for (size_t i = 0; i < ctx->ws.size(); i++)
+            if (ctx->ws[i]->stream == (hipStream_t)stream) {
+                w = ctx->ws[i];
+                ctx->ws.erase(ctx->ws.begin() + (long)i);
+                if (ctx->last_ws == w) ctx->last_ws = nullptr;
+                break;
+            }
+    }
+    if (!w) return AUTHJX_OK;
+    (void)hipSetDevice(ctx->device);
+    {
+        std::lock_guard<std::mutex> g(w->mu);  // (a call still inside on that stream finishes first)
+    }
+    destroy_workspace(w);  // (waits for the stream's last batch)
+    return AUTHJX_OK;
+}
+
 namespace {
 int finish_compile(authjx_ctx* ctx, authjx_ruleset* rs, int rc, const std::string& err, authjx_ruleset** out,
                    int32_t* pattern_status, char* errbuf, size_t errcap);

@@ -51,6 +51,7 @@ EXPORTS = [
     "authjx_eval_batch_device", "authjx_eval_batch", "authjx_last_kernel_ms", "authjx_set_exact_scan",
     "authjx_last_exact_count", "authjx_select_batch_device", "authjx_select_batch", "authjx_compile_forest",
     "authjx_select_from_eval_device", "authjx_select_text_batch_device", "authjx_select_text_batch",
+    "authjx_release_stream",
     "authjx_ruleset_trees", "authjx_batcher_create", "authjx_batcher_destroy", "authjx_batcher_eval",
     "authjx_batcher_stats",
     "authjx_index_new", "authjx_index_free", "authjx_index_set", "authjx_index_delete_key", "authjx_index_get",
@@ -368,6 +369,13 @@ class Context:
             C.c_void_p(offs.ctypes.data), C.c_void_p(lens.ctypes.data), n, C.c_void_p(out.ctypes.data), stride)
         _check(rc, "authjx_select_batch")
         return out[:n]
+
+    def release_stream(self, stream) -> None:
+        """authjx_release_stream: free the workspace kept for a (short-lived) stream."""
+        L = load_library()
+        L.authjx_release_stream.argtypes = [C.c_void_p, C.c_void_p]
+        L.authjx_release_stream.restype = C.c_int
+        _check(L.authjx_release_stream(self._h, C.c_void_p(stream)), "authjx_release_stream")
 
     def close(self):
         if getattr(self, "_h", None):

@@ -130,6 +130,10 @@ typedef struct {
  * evaluated); their handles are invalid afterwards. */
 int authjx_init(int device, authjx_ctx** out);
 void authjx_shutdown(authjx_ctx* ctx);
+/* Release the per-stream workspace (capture rows, slow list, order, set table) the
+ * context keeps for `stream` since its first device call on it, after that stream's last
+ * batch: for callers that use short-lived streams. Not the context's own stream. */
+int authjx_release_stream(authjx_ctx* ctx, void* stream);
 // The sha256 (first 32 hex digits) of the sources the library was built from
 // (authorino_amd/build.py source_hash); the Python runtime refuses a stale binary.
 const char* authjx_build_hash(void);

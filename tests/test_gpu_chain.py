@@ -97,3 +97,32 @@ def test_shutdown_destroys_live_batchers():
     ctx.close()
     assert b._h is None
     b.close()  # (a no-op now)
+
+
+def test_release_stream_workspace():
+    """authjx_release_stream (one workspace per stream handle, kept until
+    shutdown): a short-lived stream's workspace is freed after its batch; evaluating on
+    a new stream afterwards still gives the oracle's results."""
+    import torch
+
+    from authorino_amd import runtime
+
+    ctx = runtime.Context(0)
+    rs = ctx.compile([("a", 1, "x")], [(0, -1, -1, 0)], 0)
+    docs = [b'{"a":"x"}', b'{"a":"y"}'] * 64
+    arena = np.frombuffer(b"".join(docs) + b"\0", dtype=np.uint8)
+    lens = np.array([len(d) for d in docs], dtype=np.uint32)
+    offs = np.zeros(len(docs), dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1])
+    dev = torch.device("cuda:0")
+    A = torch.from_numpy(arena.copy()).to(dev)
+    Of = torch.from_numpy(offs.view(np.int64).copy()).to(dev)
+    Ln = torch.from_numpy(lens.view(np.int32).copy()).to(dev)
+    for _ in range(3):
+        s = torch.cuda.Stream()
+        tri = torch.zeros(len(docs), dtype=torch.uint8, device=dev)
+        ctx.eval_device([rs], A, Of, Ln, tri, stream=s.cuda_stream)
+        s.synchronize()
+        assert tri.cpu().numpy().tolist() == [runtime.T, runtime.F] * 64
+        ctx.release_stream(s.cuda_stream)
+    ctx.close()
