@@ -87,9 +87,11 @@ struct authjx_ctx {
     int len_sort = 1;         // order requests by length class before the single-pass kernel
     int no_tenant_stage = 0;  // profiling: multi-tenant batches read tables from global memory
     int force_scan = 0;
-    int ablate = 0;  // profiling only: 40 the token-scanner single-pass kernel, 41 the row
-                     // kernel without the exact scan after it, 1..3 / 10..12 token-scanner
-                     // ablations and workgroup sizes
+    int ablate = 0;  // profiling / comparison only: 41 the lean single-pass kernel where the
+                     // streaming kernel would run, 40 the token-scanner single-pass kernel,
+                     // 50 / 51 the streaming kernel's structural pass alone / without stage
+                     // B, 1..3 / 10..12
+                     // token-scanner ablations and workgroup sizes
 };
 
 namespace {
@@ -432,15 +434,18 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         if (rc != AUTHJX_OK) return rc;
     }
     HIP_OK(hipEventRecord(w->ev0, s));
-    // kernel: the lean single-pass kernel (ajx_lean.h; ablate 40: the token scanner of
-    // ajx_fast.h), the exact scan for what it hands over
+    // kernel: the streaming kernel (ajx_stream.h) for a one-ruleset batch whose ruleset it
+    // takes, else the lean single-pass kernel (ajx_lean.h; ablate 40: the token scanner of
+    // ajx_fast.h) or the multi-tenant kernel; the exact scan for what they hand over
     bool mods = false;  // modifier chains: the exact scan's instance with text buffers
     for (uint32_t i = 0; i < n_sets; i++)
         mods = mods || reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->n_modifiers != 0 ||
                (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagBufs) != 0;
-    // capture rows kept for authjx_select_from_eval_device: one ruleset, a full kernel
-    const bool full = ablate == 0 || ablate == 40 || (ablate >= 10 && ablate <= 12);
-    const bool keep_rows = !force_scan && n_sets == 1 && full;
+    // capture rows kept for authjx_select_from_eval_device: one forest ruleset
+    // (authjx_compile_forest), a full kernel
+    const bool full = ablate == 0 || ablate == 40 || ablate == 41 || (ablate >= 10 && ablate <= 12);
+    const auto* h0 = reinterpret_cast<const ajx::RulesetHdr*>(sets[0]->c.blob.data());
+    const bool keep_rows = !force_scan && n_sets == 1 && full && h0->pad1[0] != 0;
     w->rows_rs = keep_rows ? sets[0] : nullptr;
     w->rows_n = n;
     w->rows_stride = row_stride;
@@ -451,6 +456,14 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     if (force_scan) {
         HIP_OK(ajx::launch_eval_scan(w->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, s, mods));
+    } else if (n_sets == 1 && (ablate == 0 || ablate == 50 || ablate == 51) &&
+               ajx::stream_eligible(sets[0]->c.blob.data(), (uint32_t)sets[0]->c.blob.size())) {
+        // the streaming kernel (ajx_stream.h; ablate 50: its structural pass alone, 51: no
+        // stage B)
+        HIP_OK(ajx::launch_eval_stream(w->d_sets, (uint32_t)sets[0]->c.blob.size(), sets[0]->c.n_selectors, d_arena,
+                                       d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap,
+                                       bitmap_stride_words, keep_rows ? w->d_rows : nullptr, row_stride, w->d_slow,
+                                       w->d_slow + 1, s, ablate == 50 ? 1 : ablate == 51 ? 2 : 0, mods));
     } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
         // caller's bucketing by AuthConfig), a full kernel, batches worth sorting

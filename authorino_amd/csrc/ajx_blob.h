@@ -213,7 +213,8 @@ struct RulesetHdr {
     uint32_t key_probes;        // every key sits within key_probes slots of its home slot
     uint32_t key_mult;          // key_slot_hash multiplier
     uint32_t off_eager;         // EagerSel[n_selectors] (0: none)
-    uint32_t pad2[2];
+    uint32_t off_stream;        // StreamHdr (0: the streaming scan can not take this ruleset)
+    uint32_t pad2;
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
     uint64_t unsupported[2];    // pattern p can not be decided on the device
@@ -233,5 +234,43 @@ struct EagerSel {
 };
 static_assert(sizeof(EagerSel) == 48, "EagerSel layout");
 constexpr uint32_t kEagerValid = 1u << 31;  // a selector builds a text (a '#' list): the exact scan's buffers
+
+// ---- streaming scan (ajx_stream.h) ------------------------------------------------
+// The stream resolves object keys without their parent: every distinct object key of the
+// trie has an id 1..kStreamMaxKeys (0: not a key of any selector). A key of the document
+// at depth L is then named by the ids of the keys its containers were opened under
+// (levels 2..L) followed by its own: the path bytes, byte j = component j + 1. A selector
+// is found where those bytes equal its components' ids (the path table). Rulesets the
+// stream takes: the single-pass path's (kFlagFastOk), selectors of at most
+// kStreamMaxComps object keys (no array indices), keys of at most kStreamMaxKeyLen bytes.
+constexpr uint32_t kStreamMaxKeys = 250;
+constexpr uint32_t kStreamMaxComps = 8;
+constexpr uint32_t kStreamMaxKeyLen = 64;
+constexpr uint32_t kStreamElem = 0xFE;  // the id of an array element's container
+
+struct StreamKeySlot {
+    uint64_t sig;      // key_signature(key)
+    uint32_t meta;     // key_len | id << 16; kEmptySlot = free
+    uint32_t key_off;  // key bytes in the literal pool
+};
+struct StreamPathSlot {
+    uint64_t path;     // component ids, byte j = component j + 1
+    uint32_t meta;     // selector (0xFFFF: none) | kStreamHasKids | 1 << 31; 0 = free
+    uint32_t pad;
+};
+constexpr uint32_t kStreamHasKids = 1u << 30;  // a path node with keys below it
+static_assert(sizeof(StreamKeySlot) == 16 && sizeof(StreamPathSlot) == 16, "stream slot layout");
+
+struct StreamHdr {
+    uint32_t off_keys, key_log2, key_mult, key_probes;      // StreamKeySlot[1 << key_log2]
+    uint32_t off_paths, path_log2, path_mult, path_probes;  // StreamPathSlot[1 << path_log2]
+    uint32_t n_keys, max_key_len, pad[2];
+};
+
+AJX_BLOB_HD inline uint32_t stream_path_hash(uint64_t p, uint32_t log2, uint32_t mult) {
+    uint32_t x = (uint32_t)p ^ (((uint32_t)(p >> 32) << 11) | ((uint32_t)(p >> 32) >> 21));
+    x *= mult;
+    return x >> (32 - log2);
+}
 
 }  // namespace ajx

@@ -815,6 +815,114 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 std::memcpy(b.blob.data() + hdr.off_trie_nodes, tn.data(), tn.size() * sizeof(TrieNode));
             }
         }
+        // streaming scan tables (ajx_stream.h): key ids, and the selectors by their
+        // component ids
+        bool stream_ok = fast_ok && trie[0].selector < 0;
+        for (const Selector& s : sels) stream_ok = stream_ok && s.comp_count <= kStreamMaxComps;
+        for (const Component& c : comps) stream_ok = stream_ok && c.array_index < 0 && c.lit_len <= kStreamMaxKeyLen;
+        if (stream_ok) {
+            std::map<std::string, uint32_t> key_id;
+            std::vector<std::pair<uint64_t, uint32_t>> paths;  // (path bytes, selector)
+            uint32_t max_len = 0;
+            struct Walk {
+                uint32_t node;
+                uint64_t path;
+                uint32_t depth;
+            };
+            std::vector<Walk> stack{{0u, 0ull, 0u}};
+            while (!stack.empty() && stream_ok) {
+                const Walk w = stack.back();
+                stack.pop_back();
+                // (a node's meta: its selector, 0xFFFF none; kStreamHasKids when keys go on below it)
+                if (w.node && (trie[w.node].selector >= 0 || !trie[w.node].kids.empty()))
+                    paths.push_back({w.path, (trie[w.node].selector >= 0 ? (uint32_t)trie[w.node].selector : 0xFFFFu) |
+                                                 (trie[w.node].kids.empty() ? 0u : kStreamHasKids)});
+                for (size_t j = 0; j < trie[w.node].kids.size(); j++) {
+                    const std::string& key = trie[w.node].keys[j].first;
+                    auto it = key_id.find(key);
+                    if (it == key_id.end()) it = key_id.emplace(key, (uint32_t)key_id.size() + 1).first;
+                    max_len = std::max(max_len, (uint32_t)key.size());
+                    if (it->second > kStreamMaxKeys || w.depth >= kStreamMaxComps) {
+                        stream_ok = false;
+                        break;
+                    }
+                    stack.push_back({trie[w.node].kids[j], w.path | ((uint64_t)it->second << (8 * w.depth)), w.depth + 1});
+                }
+            }
+            if (stream_ok) {
+                // key slots: (sig, len) -> id; key bytes in the literal pool for the head compare
+                struct KEnt {
+                    uint64_t sig;
+                    uint32_t len, id, off;
+                };
+                std::vector<KEnt> kents;
+                for (const auto& kv : key_id) {
+                    while (lits.size() % 8) lits.push_back('\0');
+                    const uint32_t off = (uint32_t)lits.size();
+                    lits += kv.first;
+                    kents.push_back({key_signature((const uint8_t*)kv.first.data(), (uint32_t)kv.first.size()),
+                                     (uint32_t)kv.first.size(), kv.second, off});
+                }
+                // open addressing: the multiplier (and size) with the fewest probes
+                auto best_table = [](size_t n_ents, auto place, uint32_t& lg_out, uint32_t& mult_out,
+                                     uint32_t& probes_out) {
+                    uint32_t lg = 3;
+                    while ((1u << lg) < 2 * n_ents) lg++;
+                    uint32_t probes = 0xFFFFFFFFu;
+                    for (uint32_t l2 = lg; l2 <= lg + 2 && probes > 1; l2++) {
+                        uint32_t m = 0x9E3779B1u;
+                        for (int t = 0; t < 512 && probes > 1; t++) {
+                            const uint32_t worst = place(l2, m, false);
+                            if (worst < probes) probes = worst, lg_out = l2, mult_out = m;
+                            m = (m * 0x2C1B3C6Du + 0x297A2D38u) | 1u;
+                        }
+                    }
+                    probes_out = probes;
+                };
+                std::vector<StreamKeySlot> kslots;
+                auto place_keys = [&](uint32_t lg, uint32_t m, bool keep) -> uint32_t {
+                    std::vector<StreamKeySlot> out(1u << lg, StreamKeySlot{0, kEmptySlot, 0});
+                    uint32_t worst = 1;
+                    for (const KEnt& e : kents) {
+                        uint32_t at = key_slot_hash(e.sig, e.len, 0, lg, m), dist = 1;
+                        while (out[at].meta != kEmptySlot) at = (at + 1) & ((1u << lg) - 1), dist++;
+                        out[at] = StreamKeySlot{e.sig, e.len | (e.id << 16), e.off};
+                        worst = std::max(worst, dist);
+                    }
+                    if (keep) kslots = out;
+                    return worst;
+                };
+                std::vector<StreamPathSlot> pslots;
+                auto place_paths = [&](uint32_t lg, uint32_t m, bool keep) -> uint32_t {
+                    std::vector<StreamPathSlot> out(1u << lg, StreamPathSlot{0, 0, 0});
+                    uint32_t worst = 1;
+                    for (const auto& pe : paths) {
+                        uint32_t at = stream_path_hash(pe.first, lg, m), dist = 1;
+                        while (out[at].meta != 0) at = (at + 1) & ((1u << lg) - 1), dist++;
+                        out[at] = StreamPathSlot{pe.first, pe.second | (1u << 31), 0};
+                        worst = std::max(worst, dist);
+                    }
+                    if (keep) pslots = out;
+                    return worst;
+                };
+                StreamHdr sh;
+                std::memset(&sh, 0, sizeof sh);
+                best_table(kents.size(), place_keys, sh.key_log2, sh.key_mult, sh.key_probes);
+                place_keys(sh.key_log2, sh.key_mult, true);
+                best_table(paths.size(), place_paths, sh.path_log2, sh.path_mult, sh.path_probes);
+                place_paths(sh.path_log2, sh.path_mult, true);
+                sh.n_keys = (uint32_t)kents.size();
+                sh.max_key_len = max_len;
+                hdr.off_stream = (uint32_t)b.align16();
+                b.append(&sh, sizeof sh);
+                StreamHdr* shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
+                shp->off_keys = (uint32_t)b.align16();
+                b.append(kslots.data(), kslots.size() * sizeof(StreamKeySlot));
+                shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
+                shp->off_paths = (uint32_t)b.align16();
+                b.append(pslots.data(), pslots.size() * sizeof(StreamPathSlot));
+            }
+        }
         std::vector<SelectorPatterns> sp(sels.size());
         std::vector<uint16_t> plist;
         for (size_t s = 0; s < sels.size(); s++) {

@@ -16,6 +16,7 @@
 #include "ajx_fast.h"
 #include "ajx_lean.h"
 #include "ajx_modifiers.h"
+#include "ajx_stream.h"
 #include "ajx_kernels.h"
 
 namespace ajx {
@@ -524,6 +525,110 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
             slow_ids[atomicAdd(slow_count, 1u)] = r;
         }
     }
+}
+
+// The streaming kernel (ajx_stream.h): each wave takes a span of stream::kSpan requests in
+// arena order and reads their bytes as one coalesced stream, then runs stage B for its
+// span's requests (a lane each) on the capture rows it built in LDS. Requests it can not
+// prove go to the slow list (the exact scan). rows_out (forest rulesets, for
+// authjx_select_from_eval_device): every request's row in the wave-interleaved layout at
+// work-item r (kRowSlow for the slow ones). Profiling: MODE 1 the structural pass only, 2
+// no stage B.
+// Dynamic LDS: [blob copy] [per wave: WaveLds, capture rows, eager decisions]
+template <int MODE>
+__global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __restrict__ sets,
+                                                       const uint8_t* __restrict__ arena,
+                                                       const uint64_t* __restrict__ offs,
+                                                       const uint32_t* __restrict__ lens, uint32_t n,
+                                                       uint32_t* __restrict__ slow_count,
+                                                       uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
+                                                       int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
+                                                       uint32_t stride, uint32_t wave_off, uint32_t wave_bytes,
+                                                       uint64_t* __restrict__ rows_out, uint32_t row_stride) {
+    const uint8_t* blob = stage_blob<true>(sets[0]);
+    extern __shared__ uint4 s_stream_dyn[];
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    uint8_t* base = reinterpret_cast<uint8_t*>(s_stream_dyn) + wave_off + w * wave_bytes;
+    stream::WaveLds& L = *reinterpret_cast<stream::WaveLds*>(base);
+    uint64_t* rows = reinterpret_cast<uint64_t*>(base + sizeof(stream::WaveLds));
+    const uint32_t span = blockIdx.x * (blockDim.x >> 6) + w;
+    if (span * stream::kSpan >= n) return;  // (wave-uniform)
+    const bool ok =
+        stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm, stride);
+    const uint32_t r = span * stream::kSpan + l;
+    if (l >= stream::kSpan || r >= n) return;
+    if (!ok) slow_ids[atomicAdd(slow_count, 1u)] = r;
+    if (rows_out) {
+        const uint32_t ns = reinterpret_cast<const RulesetHdr*>(blob)->n_selectors;
+        const uint64_t* row = rows + (size_t)l * (1u + ns);
+        const RowRef o = wave_row(rows_out, row_stride, r);
+        o[0] = ok ? row[0] : kRowSlow;
+        if (ok)
+            for (uint32_t s = 0; s < ns; s++) o[1u + s] = row[1u + s];
+    }
+}
+
+bool stream_eligible(const uint8_t* host_blob, uint32_t blob_bytes) {
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(host_blob);
+    return h->off_stream != 0 && blob_bytes <= kMaxSharedBlobBytes && (h->flags & kFlagFastOk) &&
+           h->n_selectors <= kFastMaxSelectors;
+}
+
+// workgroup of 4 or 8 waves: the size that fits the most waves per CU next to the blob copy
+static uint32_t stream_block(uint32_t blob_bytes, uint32_t wave_bytes) {
+    const uint32_t stage = (blob_bytes + 15u) & ~15u;
+    uint32_t best = 256, best_w = 0;
+    for (uint32_t b = 256; b <= 512; b *= 2) {
+        const uint32_t lds = stage + (b / 64) * wave_bytes;
+        uint32_t wv = lds <= 160u * 1024u ? (160u * 1024u / lds) * (b / 64) : 0u;
+        if (wv > 32) wv = 32;
+        if (wv > best_w) best = b, best_w = wv;
+    }
+    return best;
+}
+
+hipError_t launch_eval_stream(const uint8_t* const* d_sets, uint32_t blob_bytes, uint32_t n_selectors,
+                              const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                              uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows_out,
+                              uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
+                              int mode, bool mods) {
+    if (n == 0) return hipSuccess;
+    const uint32_t wave_off = (blob_bytes + 15u) & ~15u;
+    const uint32_t wave_bytes = (stream::lds_bytes(n_selectors) + 15u) & ~15u;
+    const uint32_t block = stream_block(blob_bytes, wave_bytes);
+    const uint32_t lds = wave_off + (block / 64) * wave_bytes;
+    if (lds > 160u * 1024u) return hipErrorInvalidValue;
+    const uint32_t spans = (n + stream::kSpan - 1) / stream::kSpan;
+    const uint32_t grid = (spans + block / 64 - 1) / (block / 64);
+    hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    static std::atomic<uint64_t> attr_done{0};
+    e = attr_once(attr_done, [] {
+        for (const void* k : {reinterpret_cast<const void*>(&ajx_scan_stream<0>),
+                              reinterpret_cast<const void*>(&ajx_scan_stream<1>),
+                              reinterpret_cast<const void*>(&ajx_scan_stream<2>)}) {
+            const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (r != hipSuccess) return r;
+        }
+        return hipSuccess;
+    });
+    if (e != hipSuccess) return e;
+    if (mode == 1)
+        hipLaunchKernelGGL(ajx_scan_stream<1>, dim3(grid), dim3(block), lds, stream, d_sets, d_arena, d_offs, d_lens,
+                           n, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes, nullptr, 0u);
+    else if (mode == 2)
+        hipLaunchKernelGGL(ajx_scan_stream<2>, dim3(grid), dim3(block), lds, stream, d_sets, d_arena, d_offs, d_lens,
+                           n, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes, nullptr, 0u);
+    else
+        hipLaunchKernelGGL(ajx_scan_stream<0>, dim3(grid), dim3(block), lds, stream, d_sets, d_arena, d_offs, d_lens,
+                           n, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes, d_rows_out,
+                           row_stride);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (mode != 0) return hipSuccess;
+    const uint32_t sgrid = spans < 1024 ? 2 * ((spans * 64 + 255) / 256) : 4096;
+    launch_slow_list(mods, sgrid, stream, d_sets, nullptr, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids, d_tri,
+                     d_err, d_bm, stride);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------

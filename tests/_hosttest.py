@@ -232,3 +232,31 @@ def json_valid(text) -> int:
     """gjson Valid as the device restates it: 1 / 0, -1 undecided (nesting > 256)."""
     d = _b(text)
     return lib().ht_json_valid(d, len(d))
+
+
+def eval_stream(hr, arena, offs, lens, mode=0, stride=2, dbg=None):
+    """The streaming scan (ajx_stream.h) over a batch on the host emulation of the wave:
+    (tri, err, bitmap, slow) — slow[r] = 1 where it hands request r to the exact scan; None
+    when the ruleset has no stream tables."""
+    L = lib()
+    if not getattr(L, "_stream_decl", False):
+        L.ht_eval_stream.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]
+        L.ht_eval_stream.restype = C.c_int
+        L._stream_decl = True
+    import numpy as np
+
+    n = len(lens)
+    a = np.concatenate([np.asarray(arena, dtype=np.uint8), np.zeros(64, np.uint8)])
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    tri = np.full(n, 0xEE, np.uint8)
+    err = np.full(n, -7, np.int32)
+    bm = np.zeros((n, stride), np.uint64)
+    slow = np.zeros(n, np.uint8)
+    rc = L.ht_eval_stream(hr._h, a.ctypes.data, offs.ctypes.data, lens.ctypes.data, n, tri.ctypes.data,
+                          err.ctypes.data, bm.ctypes.data, stride, slow.ctypes.data, mode,
+                          None if dbg is None else dbg.ctypes.data)
+    if rc < 0:
+        return None
+    return tri, err, bm, slow

@@ -309,3 +309,44 @@ extern "C" void ht_lean_counts(uint64_t* iters, uint64_t* subs) {
     *iters = lean::g_lean_iters;
     *subs = lean::g_lean_subs;
 }
+
+// ---- the streaming scan (ajx_stream.h) on 64 host threads per wave (ajx_wave.h) ----
+#include "../../authorino_amd/csrc/ajx_stream.h"
+
+// every request of the batch through the stream kernel's code, one span (wave) at a time;
+// out_slow[r] = 1 where the stream hands the request to the exact scan (outputs unset).
+// mode 1: structure only (out_tri[r] = proved). Returns -1 when the ruleset has no stream
+// tables.
+extern "C" int ht_eval_stream(void* h, const uint8_t* arena, const uint64_t* offs, const uint32_t* lens, uint32_t n,
+                              uint8_t* out_tri, int32_t* out_err, uint64_t* out_bm, uint32_t stride, uint8_t* out_slow,
+                              int mode, uint32_t* out_dbg) {
+    const std::vector<uint8_t>& blob_v = ((HtRuleset*)h)->c.blob;
+    const RulesetHdr* hd = (const RulesetHdr*)blob_v.data();
+    if (!hd->off_stream) return -1;
+    // (16-byte aligned copy, as in LDS)
+    std::vector<uint64_t> blob_buf((blob_v.size() + 7) / 8 + 2);
+    std::memcpy(blob_buf.data(), blob_v.data(), blob_v.size());
+    const uint8_t* blob = (const uint8_t*)blob_buf.data();
+    const uint32_t ns = hd->n_selectors;
+    const uint32_t spans = (n + stream::kSpan - 1) / stream::kSpan;
+    std::vector<uint64_t> wl(stream::lds_bytes(ns) / 8 + 2);
+    for (uint32_t span = 0; span < spans; span++) {
+        std::memset(wl.data(), 0xA5, wl.size() * 8);
+        stream::WaveLds& L = *reinterpret_cast<stream::WaveLds*>(wl.data());
+        uint64_t* rows = wl.data() + sizeof(stream::WaveLds) / 8;
+        wave::run_wave([&](uint32_t l) {
+            bool ok;
+            if (mode == 1)
+                ok = stream::scan_span<1>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm, stride);
+            else
+                ok = stream::scan_span<0>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm, stride);
+            const uint32_t r = span * stream::kSpan + l;
+            if (l < stream::kSpan && r < n) out_slow[r] = ok ? 0 : 1;
+            if (l < stream::kSpan && r < n && out_dbg) {  // (bad position, root close)
+                out_dbg[2 * r] = L.bad[l];
+                out_dbg[2 * r + 1] = L.root_end[l];
+            }
+        });
+    }
+    return 0;
+}

@@ -1,0 +1,174 @@
+"""CPU tests of the streaming kernel's code (authorino_amd/csrc/ajx_stream.h) on its host
+build: every wave is run on 64 host threads (ajx_wave.h's emulation of ballots, lane
+shifts and scans), and its decisions are compared bit for bit with the oracle (tri-state,
+error index, pattern bitmap) wherever it does not hand a request to the exact scan.
+
+Inputs: the bench workloads' documents (all proved, none handed over), random compact
+documents with random selectors, mutated documents (soundness: a document the stream
+proves must give the oracle's answer), documents at every byte alignment and across step
+boundaries, and hand-written invalid documents the stream must not prove."""
+import json
+
+import numpy as np
+import pytest
+
+import _hosttest as H
+import fuzz_util as FU
+import pyoracle as O
+
+
+def _pack(docs):
+    lens = np.array([len(d) for d in docs], dtype=np.uint32)
+    offs = np.zeros(len(docs), dtype=np.uint64)
+    if len(docs):
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    arena = np.frombuffer(b"".join(docs), dtype=np.uint8).copy() if docs else np.zeros(0, np.uint8)
+    return arena, offs, lens
+
+
+def _check(pats, nodes, root, arena, offs, lens, allow_slow=True):
+    """The stream's answers equal the oracle's where it decides; returns the slow mask
+    (None: the ruleset has no stream tables)."""
+    hr = H.HostRuleset(pats, nodes, root)
+    assert hr.rc == 0, hr.error
+    res = H.eval_stream(hr, arena, offs, lens)
+    if res is None:
+        return None
+    tri, err, bm, slow = res
+    rs = O.Ruleset(pats, nodes, root)
+    otri, oerr, obm = O.eval_batch([rs], arena, offs, lens)
+    ok = slow == 0
+    np.testing.assert_array_equal(tri[ok], otri[ok])
+    np.testing.assert_array_equal(err[ok], oerr[ok])
+    np.testing.assert_array_equal(bm[ok, :obm.shape[1]], obm[ok])
+    if not allow_slow:
+        assert not slow.any(), np.nonzero(slow)[0]
+    return slow.astype(bool)
+
+
+def _flat(expr):
+    pats, nodes, root = expr.flatten()
+    return [(p.selector, int(p.operator), p.value) for p in pats], nodes, root
+
+
+@pytest.mark.parametrize("wl,n", [("c2", 256), ("c5", 96)])
+def test_stream_workloads_match_oracle(wl, n):
+    """The bench documents: every one proved (no exact-scan hand-over), bit-exact."""
+    from authorino_amd import workloads
+
+    w = workloads.make(wl, n=n, unique=n)
+    exprs = [w.expr] if wl == "c2" else [w.auth_config.conditions] + [
+        e for c in w.auth_config.authorization for e in (c.conditions, c.rules)]
+    for e in exprs:
+        slow = _check(*_flat(e), w.arena, w.offs, w.lens, allow_slow=False)
+        assert slow is not None
+
+
+def test_stream_every_alignment_and_step_boundary():
+    """The same documents at all 32 byte alignments of the arena and with long fillers
+    that put keys, values and containers across lane and step boundaries."""
+    from authorino_amd import workloads
+
+    w = workloads.make("c2", n=48, unique=48)
+    rng = np.random.default_rng(7)
+    docs = []
+    for i in range(w.n):
+        d = w.doc(i)
+        if i % 3 == 0:  # a filler key of 1..2100 bytes in front: everything after it shifts
+            pad = '"zz%d":"%s",' % (i, "q" * int(rng.integers(1, 2100)))
+            d = d[:1] + pad.encode() + d[1:]
+        docs.append(d)
+    for shift in range(0, 32, 3):
+        a, o, ln = _pack([b"x" * shift] + docs)
+        slow = _check(*_flat(w.expr), a, o[1:], ln[1:], allow_slow=False)
+        assert slow is not None
+
+
+def _stream_patterns(rng, k):
+    while True:
+        pats = FU.rand_patterns(rng, k)
+        if all(not any(part.isdigit() for part in p[0].split(".")) for p in pats):
+            return pats
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_stream_random_documents(seed):
+    """Random compact documents and selectors: bit-exact where decided, and compact valid
+    documents are nearly all decided."""
+    rng = np.random.default_rng(400 + seed)
+    decided = total = 0
+    for _ in range(6):
+        pats = _stream_patterns(rng, int(rng.integers(1, 7)))
+        nodes, root = FU.chain(len(pats))
+        docs = [FU.rand_doc(rng, ws=False) for _ in range(64)]
+        a, o, ln = _pack(docs)
+        slow = _check(pats, nodes, root, a, o, ln)
+        if slow is None:
+            continue
+        decided += int((~slow).sum())
+        total += len(docs)
+    assert total == 0 or decided >= total // 2
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_stream_mutated_documents_are_sound(seed):
+    """Truncated, byte-flipped, whitespace-padded documents: whatever the stream decides
+    equals the oracle (which restates gjson on any input)."""
+    rng = np.random.default_rng(500 + seed)
+    for _ in range(6):
+        pats = _stream_patterns(rng, int(rng.integers(1, 6)))
+        nodes, root = FU.chain(len(pats))
+        docs = [FU.mutate(rng, FU.rand_doc(rng, ws=False)) for _ in range(64)]
+        _check(pats, nodes, root, *_pack(docs))
+
+
+INVALID = [
+    b'{"a","b":"v"}', b'{"a":1,"b"}', b'{"a":1,2}', b'["a":1]', b'{"a"}', b'{{}}', b'{"a":{},{}}',
+    b'{"a":"b":"v"}', b'{"a":[1}', b'{"a":[1]]}', b'{"b":{"a":1]}', b'{"a":1}}', b'{"a":1', b'{"a" :1}',
+    b' {"a":1}', b'{"a":tru}', b'{"a":1,}', b'{,"a":1}', b'{"a":(1)}', b'{"a":[1,{"b":2]]}', b'{"a\\u0062":1}',
+    b'{"a":"x"' + b'"y"}', b'{"a":1}' + b'{"b":2', b'[{"a":1},"b":2]', b'{"a":x}',
+    b'{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":{"a":1}}}}}}}}}}}}}}}}}',
+]
+
+
+def test_stream_invalid_documents_go_to_the_exact_scan():
+    """Documents the stream must not prove (object alternation, kinds, depth, escapes in
+    keys, whitespace, inexact literals, ...) are handed over — or, where the problem lies
+    after the root's close, decided like the oracle."""
+    pats = [("a", 1, "1"), ("b", 2, "v"), ("a.b", 1, "2"), ("a.a.a", 3, "x")]
+    nodes, root = FU.chain(len(pats))
+    docs = INVALID * 3
+    slow = _check(pats, nodes, root, *_pack(docs))
+    assert slow is not None
+    after_root = {b'{"a":1}' + b'{"b":2', b'{"a":1}}'}
+    for d, s in zip(docs, slow):
+        if d not in after_root:
+            assert s, d
+
+
+def test_stream_keys_with_escapes_and_long_values():
+    """A key that needs unescaping, keys and values longer than a lane or a step, strings
+    with escaped quotes and backslashes right at lane boundaries."""
+    rng = np.random.default_rng(11)
+    pats = [("k", 1, "v"), ("long-key-name-%s" % ("x" * 40), 1, "w"), ("s", 2, 'a"b'), ("t.u", 3, "e")]
+    nodes, root = FU.chain(len(pats))
+    docs = []
+    for i in range(128):
+        pad = "p" * int(rng.integers(0, 90))
+        val = "\\\\" * int(rng.integers(0, 4)) + '\\"' * int(rng.integers(0, 3)) + "q" * int(rng.integers(0, 40))
+        parts = ['"pad":"%s"' % pad, '"s":"%s"' % val, '"k":"%s"' % ("v" if i % 2 else "w" * (i % 37)),
+                 '"long-key-name-%s":"w"' % ("x" * 40), '"t":{"u":["e","f%s"]}' % ("g" * (i % 50))]
+        if i % 5 == 0:
+            parts.append('"k\\u0020":"v"')
+        rng.shuffle(parts)
+        docs.append(("{" + ",".join(parts) + "}").encode())
+    slow = _check(pats, nodes, root, *_pack(docs))
+    assert slow is not None
+    assert not slow[[i for i in range(128) if i % 5]].any()
+
+
+def test_stream_empty_and_tiny_documents():
+    pats = [("a", 1, "1"), ("b", 4, "x")]
+    nodes, root = FU.chain(len(pats))
+    docs = [b"", b"{}", b"[]", b'{"a":1}', b"1", b'"a"', b"{", b'{"a":1}' * 2, b'{"a":[]}', b'{"b":["x"]}']
+    _check(pats, nodes, root, *_pack(docs))
