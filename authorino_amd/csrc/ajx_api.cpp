@@ -89,8 +89,8 @@ struct authjx_ctx {
     int force_scan = 0;
     int ablate = 0;  // profiling / comparison only: 41 the lean single-pass kernel where the
                      // streaming kernel would run, 40 the token-scanner single-pass kernel,
-                     // 50 / 51 the streaming kernel's structural pass alone / without stage
-                     // B, 1..3 / 10..12
+                     // 50 / 51 the streaming kernel's structural pass alone / without its
+                     // fold, 1..3 / 10..12
                      // token-scanner ablations and workgroup sizes
 };
 
@@ -429,8 +429,13 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     HIP_OK(hipSetDevice(ctx->device));
     int rc = ensure_sets(w, ctx->device, sets, n_sets);
     if (rc != AUTHJX_OK) return rc;
+    // the streaming kernel takes a one-ruleset batch whose ruleset has stream tables (its
+    // rows carry 4 more words: the eager decisions stage B reads)
+    const bool use_stream = !force_scan && n_sets == 1 && (ablate == 0 || ablate == 50 || ablate == 51) &&
+                            ajx::stream_eligible(sets[0]->c.blob.data(), (uint32_t)sets[0]->c.blob.size());
+    const uint32_t rows_stride = use_stream ? row_stride + 4u : row_stride;
     if (!force_scan) {
-        rc = ensure_work(w, n, row_stride);
+        rc = ensure_work(w, n, rows_stride);
         if (rc != AUTHJX_OK) return rc;
     }
     HIP_OK(hipEventRecord(w->ev0, s));
@@ -456,13 +461,13 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     if (force_scan) {
         HIP_OK(ajx::launch_eval_scan(w->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, s, mods));
-    } else if (n_sets == 1 && (ablate == 0 || ablate == 50 || ablate == 51) &&
-               ajx::stream_eligible(sets[0]->c.blob.data(), (uint32_t)sets[0]->c.blob.size())) {
+    } else if (use_stream) {
         // the streaming kernel (ajx_stream.h; ablate 50: its structural pass alone, 51: no
-        // stage B)
+        // fold), its stage B over the d_perm buffer as the stage-B list
+        w->rows_stride = rows_stride;
         HIP_OK(ajx::launch_eval_stream(w->d_sets, (uint32_t)sets[0]->c.blob.size(), sets[0]->c.n_selectors, d_arena,
                                        d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap,
-                                       bitmap_stride_words, keep_rows ? w->d_rows : nullptr, row_stride, w->d_slow,
+                                       bitmap_stride_words, w->d_rows, rows_stride, keep_rows, w->d_perm, w->d_slow,
                                        w->d_slow + 1, s, ablate == 50 ? 1 : ablate == 51 ? 2 : 0, mods));
     } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the

@@ -264,7 +264,9 @@ static_assert(sizeof(StreamKeySlot) == 16 && sizeof(StreamPathSlot) == 16, "stre
 struct StreamHdr {
     uint32_t off_keys, key_log2, key_mult, key_probes;      // StreamKeySlot[1 << key_log2]
     uint32_t off_paths, path_log2, path_mult, path_probes;  // StreamPathSlot[1 << path_log2]
-    uint32_t n_keys, max_key_len, pad[2];
+    uint32_t n_keys, max_key_len;
+    uint32_t light;  // every pattern is an eager one (EagerSel): stage B is the fold alone
+    uint32_t pad;
 };
 
 AJX_BLOB_HD inline uint32_t stream_path_hash(uint64_t p, uint32_t log2, uint32_t mult) {

@@ -913,6 +913,16 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 place_paths(sh.path_log2, sh.path_mult, true);
                 sh.n_keys = (uint32_t)kents.size();
                 sh.max_key_len = max_len;
+                // light: every pattern is one of its selector's eager patterns (the stream
+                // decides them all while it captures)
+                bool light = np <= 64 && hdr.off_eager != 0;
+                for (uint32_t i = 0; i < np && light; i++) {
+                    const Pattern& pt = pats[i];
+                    light = pt.state == P_OK && pt.lit_len <= 16 &&
+                            (pt.op == OP_EQ || pt.op == OP_NEQ || pt.op == OP_INCL || pt.op == OP_EXCL);
+                }
+                for (size_t sidx = 0; sidx < sel_pats.size() && light; sidx++) light = sel_pats[sidx].size() <= 2;
+                sh.light = light ? 1u : 0u;
                 hdr.off_stream = (uint32_t)b.align16();
                 b.append(&sh, sizeof sh);
                 StreamHdr* shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);

@@ -1055,7 +1055,10 @@ AJX_HD bool incl_hits(const uint8_t* doc, const ValueRef& v, const Pattern* pats
             else return false;
         } else if (c == '-' || (c >= '0' && c <= '9')) {
             uint32_t k = i + 1;
-            while (k < end && doc[k] != ',') k++;
+            while (k < end && doc[k] != ',') {
+                if (doc[k] <= ' ') return false;  // (gjson's number ends there: the general path)
+                k++;
+            }
             e.end = k;
             e.type = T_NUMBER;
         } else {

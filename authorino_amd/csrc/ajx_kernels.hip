@@ -528,12 +528,14 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
 }
 
 // The streaming kernel (ajx_stream.h): each wave takes a span of stream::kSpan requests in
-// arena order and reads their bytes as one coalesced stream, then runs stage B for its
-// span's requests (a lane each) on the capture rows it built in LDS. Requests it can not
-// prove go to the slow list (the exact scan). rows_out (forest rulesets, for
-// authjx_select_from_eval_device): every request's row in the wave-interleaved layout at
-// work-item r (kRowSlow for the slow ones). Profiling: MODE 1 the structural pass only, 2
-// no stage B.
+// arena order and reads their bytes as one coalesced stream; a lane per request then folds
+// the patterns the stream decided. Requests with a pattern left (a value to parse or
+// unescape, a regex, a long value) go with their row (found word, records, the 4 eager
+// words: row_stride >= 5 + n_selectors) to ajx_stream_finish through the stage-B list;
+// requests it can not prove go to the slow list (the exact scan). keep_rows (forest
+// rulesets, for authjx_select_from_eval_device): every request's row is written (slow
+// ones: kRowSlow), those with an open record through stage B. Rows: the wave-interleaved
+// layout at work-item r. Profiling: MODE 1 the structural pass only, 2 no fold.
 // Dynamic LDS: [blob copy] [per wave: WaveLds, capture rows, eager decisions]
 template <int MODE>
 __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __restrict__ sets,
@@ -541,10 +543,11 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
                                                        const uint64_t* __restrict__ offs,
                                                        const uint32_t* __restrict__ lens, uint32_t n,
                                                        uint32_t* __restrict__ slow_count,
-                                                       uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
-                                                       int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
-                                                       uint32_t stride, uint32_t wave_off, uint32_t wave_bytes,
-                                                       uint64_t* __restrict__ rows_out, uint32_t row_stride) {
+                                                       uint32_t* __restrict__ slow_ids, uint32_t* __restrict__ stage_list,
+                                                       uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                                       uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t wave_off,
+                                                       uint32_t wave_bytes, uint64_t* __restrict__ rows_out,
+                                                       uint32_t row_stride, uint32_t keep_rows) {
     const uint8_t* blob = stage_blob<true>(sets[0]);
     extern __shared__ uint4 s_stream_dyn[];
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
@@ -553,18 +556,49 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
     uint64_t* rows = reinterpret_cast<uint64_t*>(base + sizeof(stream::WaveLds));
     const uint32_t span = blockIdx.x * (blockDim.x >> 6) + w;
     if (span * stream::kSpan >= n) return;  // (wave-uniform)
-    const bool ok =
-        stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm, stride);
+    const uint64_t *rowp = nullptr, *dwp = nullptr;
+    const uint32_t res = stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm,
+                                                 stride, &rowp, &dwp);
     const uint32_t r = span * stream::kSpan + l;
-    if (l >= stream::kSpan || r >= n) return;
-    if (!ok) slow_ids[atomicAdd(slow_count, 1u)] = r;
-    if (rows_out) {
-        const uint32_t ns = reinterpret_cast<const RulesetHdr*>(blob)->n_selectors;
-        const uint64_t* row = rows + (size_t)l * (1u + ns);
-        const RowRef o = wave_row(rows_out, row_stride, r);
-        o[0] = ok ? row[0] : kRowSlow;
-        if (ok)
-            for (uint32_t s = 0; s < ns; s++) o[1u + s] = row[1u + s];
+    if (l >= stream::kSpan || r >= n || MODE != 0) return;
+    const RowRef o = wave_row(rows_out, row_stride, r);
+    if (res == stream::R_SLOW) {
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
+        if (keep_rows) o[0] = kRowSlow;
+        return;
+    }
+    const uint32_t ns = reinterpret_cast<const RulesetHdr*>(blob)->n_selectors;
+    bool open = false;
+    if (keep_rows)
+        for (uint32_t s = 0; s < ns; s++) open = open || ((rowp[1u + s] >> 32) & stream::kOpenEnd);
+    if (res == stream::R_STAGE_B || open) {
+        for (uint32_t s = 0; s <= ns; s++) o[s] = rowp[s];
+        for (uint32_t k = 0; k < 4; k++) o[1u + ns + k] = dwp[k];
+        stage_list[1u + atomicAdd(stage_list, 1u)] = r;
+    } else if (keep_rows) {
+        for (uint32_t s = 0; s <= ns; s++) o[s] = rowp[s];
+    }
+}
+
+// Stage B of the streaming kernel: one work-item per request on the stage-B list, on its
+// row in HBM (stream::finish_full); what it can not decide goes to the slow list.
+__global__ __launch_bounds__(256) void ajx_stream_finish(const uint8_t* const* __restrict__ sets,
+                                                         const uint8_t* __restrict__ arena,
+                                                         const uint64_t* __restrict__ offs,
+                                                         const uint32_t* __restrict__ lens,
+                                                         const uint32_t* __restrict__ stage_list,
+                                                         uint64_t* __restrict__ rows, uint32_t row_stride,
+                                                         uint32_t* __restrict__ slow_count,
+                                                         uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
+                                                         int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
+                                                         uint32_t stride) {
+    const uint8_t* blob = stage_blob<true>(sets[0]);
+    const uint32_t cnt = *stage_list;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+        const uint32_t r = stage_list[1u + i];
+        if (!stream::finish_full(r, blob, arena + offs[r], lens[r], wave_row(rows, row_stride, r), out_tri, out_err,
+                                 out_bm, stride))
+            slow_ids[atomicAdd(slow_count, 1u)] = r;
     }
 }
 
@@ -589,10 +623,11 @@ static uint32_t stream_block(uint32_t blob_bytes, uint32_t wave_bytes) {
 
 hipError_t launch_eval_stream(const uint8_t* const* d_sets, uint32_t blob_bytes, uint32_t n_selectors,
                               const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
-                              uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows_out,
-                              uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                              int mode, bool mods) {
+                              uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
+                              uint32_t row_stride, bool keep_rows, uint32_t* d_stage_list, uint32_t* d_slow_count,
+                              uint32_t* d_slow_ids, hipStream_t stream, int mode, bool mods) {
     if (n == 0) return hipSuccess;
+    if (row_stride < 5u + n_selectors) return hipErrorInvalidValue;
     const uint32_t wave_off = (blob_bytes + 15u) & ~15u;
     const uint32_t wave_bytes = (stream::lds_bytes(n_selectors) + 15u) & ~15u;
     const uint32_t block = stream_block(blob_bytes, wave_bytes);
@@ -602,29 +637,37 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, uint32_t blob_bytes,
     const uint32_t grid = (spans + block / 64 - 1) / (block / 64);
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(d_stage_list, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
     static std::atomic<uint64_t> attr_done{0};
     e = attr_once(attr_done, [] {
         for (const void* k : {reinterpret_cast<const void*>(&ajx_scan_stream<0>),
                               reinterpret_cast<const void*>(&ajx_scan_stream<1>),
-                              reinterpret_cast<const void*>(&ajx_scan_stream<2>)}) {
+                              reinterpret_cast<const void*>(&ajx_scan_stream<2>),
+                              reinterpret_cast<const void*>(&ajx_stream_finish)}) {
             const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (r != hipSuccess) return r;
         }
         return hipSuccess;
     });
     if (e != hipSuccess) return e;
+#define AJX_STREAM_LAUNCH(M)                                                                                       \
+    hipLaunchKernelGGL((ajx_scan_stream<M>), dim3(grid), dim3(block), lds, stream, d_sets, d_arena, d_offs, d_lens, n, \
+                       d_slow_count, d_slow_ids, d_stage_list, d_tri, d_err, d_bm, stride, wave_off, wave_bytes,      \
+                       d_rows, row_stride, keep_rows ? 1u : 0u)
     if (mode == 1)
-        hipLaunchKernelGGL(ajx_scan_stream<1>, dim3(grid), dim3(block), lds, stream, d_sets, d_arena, d_offs, d_lens,
-                           n, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes, nullptr, 0u);
+        AJX_STREAM_LAUNCH(1);
     else if (mode == 2)
-        hipLaunchKernelGGL(ajx_scan_stream<2>, dim3(grid), dim3(block), lds, stream, d_sets, d_arena, d_offs, d_lens,
-                           n, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes, nullptr, 0u);
+        AJX_STREAM_LAUNCH(2);
     else
-        hipLaunchKernelGGL(ajx_scan_stream<0>, dim3(grid), dim3(block), lds, stream, d_sets, d_arena, d_offs, d_lens,
-                           n, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes, d_rows_out,
-                           row_stride);
+        AJX_STREAM_LAUNCH(0);
+#undef AJX_STREAM_LAUNCH
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mode != 0) return hipSuccess;
+    // stage B and the exact scan over their lists (grid-stride: the lists' lengths are on the device)
+    const uint32_t fgrid = spans < 2048 ? (spans * stream::kSpan + 255) / 256 : 4096;
+    hipLaunchKernelGGL(ajx_stream_finish, dim3(fgrid), dim3(256), wave_off, stream, d_sets, d_arena, d_offs, d_lens,
+                       d_stage_list, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t sgrid = spans < 1024 ? 2 * ((spans * 64 + 255) / 256) : 4096;
     launch_slow_list(mods, sgrid, stream, d_sets, nullptr, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids, d_tri,
                      d_err, d_bm, stride);

@@ -87,8 +87,10 @@ AJX_HD Stk stk_then(const Stk& a, const Stk& b) {
     return r;
 }
 
-// the wave's LDS (rows follow it: kSpan x (1 + n_selectors) words, then 2 x kSpan words of
-// eager decisions)
+// the wave's LDS (rows follow it: kSpan x (1 + n_selectors) words, then 4 words per document
+// of eager decisions: patterns decided, those of them true, array elements equal to a
+// selector's eager literals (2 bits per selector < 32), selectors whose arrays hold other
+// elements)
 struct WaveLds {
     // the ring: the step's 64 blocks at 64 + 32 l, the previous step's last two at 0 and
     // 32 (byte address a of the span's stream at ring index a - (2048 t - 64)); 16 bytes of
@@ -103,12 +105,43 @@ struct WaveLds {
 __host__ __device__
 #endif
 constexpr uint32_t lds_bytes(uint32_t n_selectors) {
-    return (uint32_t)sizeof(WaveLds) + kSpan * (1u + n_selectors) * 8u + 2u * kSpan * 8u;
+    return (uint32_t)sizeof(WaveLds) + kSpan * (1u + n_selectors) * 8u + 4u * kSpan * 8u;
 }
 
 struct alignas(16) V4 {
     uint32_t x, y, z, w;
 };
+
+// The stream's byte classes: ajx_lean.h's, with class 7 (control bytes there) replaced by
+// 0x58..0x5F, which among the brackets holds [ and ] only (their kind, for the container
+// stack). Control bytes outside strings are then scalar bytes: a scalar run may not start
+// with one (the value-start check) and a captured or parsed scalar may not hold one (the
+// captures and stage B check its bytes).
+constexpr uint32_t K_SQ = 7;
+constexpr uint32_t kSqH0[8] = {lean::kSetH0[0], lean::kSetH0[1], lean::kSetH0[2], lean::kSetH0[3], lean::kSetH0[4],
+                               lean::kSetH0[5], lean::kSetH0[6], 0xFFu};
+constexpr uint32_t kSqH1[8] = {lean::kSetH1[0], lean::kSetH1[1], lean::kSetH1[2], lean::kSetH1[3], lean::kSetH1[4],
+                               lean::kSetH1[5], lean::kSetH1[6], 1u << 3};
+constexpr uint32_t kSqH2[8] = {lean::kSetH2[0], lean::kSetH2[1], lean::kSetH2[2], lean::kSetH2[3], lean::kSetH2[4],
+                               lean::kSetH2[5], lean::kSetH2[6], 1u << 1};
+constexpr uint32_t kS0lo = lean::lut_word(kSqH0, 0), kS0hi = lean::lut_word(kSqH0, 4);
+constexpr uint32_t kS1lo = lean::lut_word(kSqH1, 0), kS1hi = lean::lut_word(kSqH1, 4);
+constexpr uint32_t kS2lo = lean::lut_word(kSqH2, 0);
+constexpr bool sq_lut_ok() {
+    for (uint32_t b = 0; b < 256; b++) {
+        const uint32_t c = lean::lut_byte(kSqH0, b & 7) & lean::lut_byte(kSqH1, (b >> 3) & 7) & lean::lut_byte(kSqH2, b >> 6);
+        const uint32_t want = (lean::class_ref(b) & 0x7Fu) | ((b >= 0x58 && b <= 0x5F) ? 0x80u : 0u);
+        if (c != want) return false;
+    }
+    return true;
+}
+static_assert(sq_lut_ok(), "stream byte-class LUT");
+AJX_HD uint32_t classify4(uint32_t x) {
+    const uint32_t a = lean::perm(kS0hi, kS0lo, x & 0x07070707u);
+    const uint32_t b = lean::perm(kS1hi, kS1lo, (x >> 3) & 0x07070707u);
+    const uint32_t c = lean::perm(0u, kS2lo, (x >> 6) & 0x03030303u);
+    return a & b & c;
+}
 
 // ring reads (index any int within the slack; unaligned)
 AJX_HD uint32_t ring32(const uint8_t* ring, int32_t a) {
@@ -255,9 +288,8 @@ AJX_HD void span_setup(WaveLds& L, uint64_t* rows, uint32_t ns, uint32_t l, bool
         // the document's capture row (records: start kNone = not found) and eager decisions
         uint64_t* row = rows + (size_t)l * (1u + ns);
         for (uint32_t s = 0; s <= ns; s++) row[s] = s ? (uint64_t)kNone : 0ull;
-        uint64_t* dec = rows + (size_t)kSpan * (1u + ns);
-        dec[2 * l] = 0;
-        dec[2 * l + 1] = 0;
+        uint64_t* dec = rows + (size_t)kSpan * (1u + ns) + 4u * l;
+        dec[0] = dec[1] = dec[2] = dec[3] = 0;
     }
     if (l < 2) L.heads[l] = 0;
     wave::sync();
@@ -338,7 +370,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
     // ---- classification (ajx_lean.h)
     uint32_t d[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) d[j] = lean::classify4(B.x[j]);
+    for (int j = 0; j < 8; j++) d[j] = classify4(B.x[j]);
     lean::transpose(d);
     const uint32_t Q = d[lean::creg(lean::K_Q)] & valid, BS = d[lean::creg(lean::K_BS)] & valid;
     uint32_t bad = 0;
@@ -401,7 +433,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
     const uint32_t outside = ~X & ~U & valid;
     const uint32_t OP = d[lean::creg(lean::K_OPEN)] & outside, CL = d[lean::creg(lean::K_CLOSE)] & outside;
     const uint32_t CO = d[lean::creg(lean::K_COLON)] & outside, CM = d[lean::creg(lean::K_COMMA)] & outside;
-    const uint32_t badb = (d[lean::creg(lean::K_BAD1)] | d[lean::creg(lean::K_CTRL)] | BS) & outside;
+    const uint32_t badb = (d[lean::creg(lean::K_BAD1)] | BS) & outside;
     const uint32_t ST = OP | CL | CO | CM;
     const uint32_t SC = outside & ~ST & ~badb;
 
@@ -461,10 +493,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
     const int32_t depth_in = ff ? Ex - ((int32_t)(ff & 0xFFFFFu) - (1 << 19)) : Ex + c.depth;
     c.depth = (int32_t)wave::readlane((uint32_t)(depth_in + net), 63);
 
-    // ---- bracket kinds ([ ] vs { }: bit 5) from the ring
-    uint32_t ARR = 0;
-    for (uint32_t m = OP | CL; m; m &= m - 1u)
-        if (!(ring[64 + 32 * l + ctz(m)] & 0x20u)) ARR |= m & (0u - m);
+    const uint32_t ARR = d[lean::creg(K_SQ)] & (OP | CL);  // [ and ]
 
     // ---- keys (ids) and brackets in document order: the lane's container transform, kind
     // and alternation checks, root close
@@ -621,23 +650,43 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
     bad = 0;
 
     if constexpr (MODE != 1) {
-        // ---- keys on selector paths: capture their values. The next lane's first bytes
-        // (a value that starts or ends there)
+        // ---- keys on selector paths: capture their values; elements of captured arrays
+        // with incl / excl patterns: compare them. The next lane's first bytes (a value that
+        // starts or ends there)
         const uint32_t fcq = CQ ? ctz(CQ) : 32u, fst = (ST & valid) ? ctz(ST & valid) : 32u;
         const uint32_t nx_info = (OQ & 1u) | ((OP & 1u) << 1) | ((SCS & 1u) << 2) | (fcq << 3) | (fst << 9) |
-                                 (((BS & below(fcq)) ? 1u : 0u) << 15) | ((head ? 1u : 0u) << 16);
+                                 (((BS & below(fcq)) ? 1u : 0u) << 15) | ((head ? 1u : 0u) << 16) |
+                                 ((CO & 1u) << 17) | ((ARR & 1u) << 18);
         const uint32_t nx = wave::shl1(nx_info, 1u << 16);  // (lane 63: as if the next were another document)
+        // element strings (closing quotes of strings neither keys nor values after ':') and
+        // element scalars, looked at only in arrays on selector paths
+        const uint32_t ELQ = T.eg ? CQ & ~Mv & ~((CO >> 1) | (((nx >> 17) & 1u) << 31)) : 0u;
+        const uint32_t ELS = T.eg ? SCS & ~nCO : 0u;
         wave::sync();  // (the ring holds every lane's block)
-        if (KEYC) {
+        if (KEYC | ELQ | ELS) {
             const uint32_t ns = T.ns;
             uint64_t* row = rows + (size_t)doc * (1u + ns);
-            uint64_t* dec = rows + (size_t)kSpan * (1u + ns) + 2u * doc;
+            uint64_t* dec = rows + (size_t)kSpan * (1u + ns) + 4u * doc;
             int32_t dd = depth_in;
             uint64_t iv = (uint64_t)stk_in.iv0 | ((uint64_t)stk_in.iv1 << 32);
             uint32_t nk = 0, no = 0;
-            for (uint32_t m = OP | CL | KEYC; m; m &= m - 1u) {
+            // the selector whose path is the container at level dd (kNone: none)
+            auto container_sel = [&]() -> uint32_t {
+                if (dd < 2 || dd > (int32_t)kStreamMaxComps + 1) return kNone;
+                const uint32_t nb = (uint32_t)dd - 1u;
+                const uint64_t keep = ~0ull >> (64u - 8u * nb);
+                const uint64_t pth = iv & keep;
+                if (((pth - 0x0101010101010101ull) & ~pth & 0x8080808080808080ull) & keep) return kNone;
+                const uint32_t pm = path_meta(T, pth);
+                return (pm && (pm & 0xFFFFu) != 0xFFFFu) ? (pm & 0xFFFFu) : kNone;
+            };
+            for (uint32_t m = OP | CL | KEYC | ELQ | ELS; m; m &= m - 1u) {
                 const uint32_t i = ctz(m);
                 if ((OP >> i) & 1u) {
+                    if (T.eg && !((nCO >> i) & 1u)) {  // a container element: its array is not all strings
+                        const uint32_t sa = container_sel();
+                        if (sa < 32u) wave::lds_or64(&dec[3], 1ull << sa);
+                    }
                     dd++;
                     if (dd >= 2 && dd <= 9) {
                         const uint32_t sh = 8u * (uint32_t)(dd - 2);
@@ -649,6 +698,36 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                 }
                 if ((CL >> i) & 1u) {
                     dd--;
+                    continue;
+                }
+                if ((ELQ | ELS) & (1u << i)) {
+                    const uint32_t sa = container_sel();
+                    if (sa >= 32u) continue;
+                    const EagerSel eg = T.eg[sa];
+                    bool simple = ((ELQ >> i) & 1u) != 0;
+                    uint32_t hit = 0;
+                    if (simple) {  // the element's text: (its opening quote, i)
+                        const uint32_t oqb = i ? OQ & below(i) : 0u;
+                        const uint32_t oqpos = oqb ? (uint32_t)(pos0 + (int32_t)hib(oqb)) : (loqv >> 1) - 1u;
+                        const uint32_t cqpos = (uint32_t)(pos0 + (int32_t)i);
+                        const uint32_t cl = cqpos - oqpos - 1u;
+                        simple = (oqb || loqv) && cqpos > oqpos &&
+                                 (cl > 16u || in_ring(roff + (int32_t)oqpos + 1, cl));
+                        if (simple && bs_keys) {  // (an escape: the exact compare of stage B)
+                            const int32_t lo = (int32_t)oqpos + 1 - pos0, hi = (int32_t)cqpos - pos0;
+                            auto bits = [](int32_t a, int32_t b) -> uint32_t {
+                                a = a < 0 ? 0 : a;
+                                b = b > 32 ? 32 : b;
+                                return a >= b ? 0u : below((uint32_t)b) & ~below((uint32_t)a);
+                            };
+                            simple = !((BS & bits(lo, hi)) || (pBS & bits(lo + 32, hi + 32)) || lo < -32);
+                        }
+                        if (simple) hit = eager_hits(eg, ring, roff + (int32_t)oqpos + 1, cl);
+                    }
+                    if (!simple)
+                        wave::lds_or64(&dec[3], 1ull << sa);
+                    else if (hit)
+                        wave::lds_or64(&dec[2], (uint64_t)hit << (2u * sa));
                     continue;
                 }
                 const uint32_t own = nk < 8 ? (uint32_t)(kids >> (8u * nk)) & 0xFFu : 0u;
@@ -670,7 +749,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                 if (!pm || s == 0xFFFFu) continue;
                 // the value: at i + 1 (this lane) or the next lane's byte 0
                 const uint32_t vpos = (uint32_t)(pos0 + (int32_t)i) + 1u;
-                uint32_t type = kTypeUnknown, end = 0, esc = 0, open = 1;
+                uint32_t type = kTypeUnknown, end = 0, esc = 0, open = 1, arr = 0;
                 if (i < 31) {
                     const uint32_t j = i + 1u;
                     if ((OQ >> j) & 1u) {
@@ -687,6 +766,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                         }
                     } else if ((OP >> j) & 1u) {
                         type = T_JSON;
+                        arr = (ARR >> j) & 1u;
                     } else if ((SCS >> j) & 1u) {
                         type = T_NUMBER;
                         const uint32_t q = ST & valid & ~below(j);
@@ -700,17 +780,44 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                     }
                 } else if (!((nx >> 16) & 1u)) {
                     type = (nx & 1u) ? T_STRING : ((nx >> 1) & 1u) ? T_JSON : ((nx >> 2) & 1u) ? T_NUMBER : kTypeUnknown;
+                    arr = type == T_JSON ? (nx >> 18) & 1u : 0u;
                 }
-                if (type == T_NUMBER && !open) {  // literals must be exact (gjson takes any letters)
-                    const int32_t ra = roff + (int32_t)vpos;
+                // the text eager patterns compare: a string's contents, a literal's or an
+                // integer's raw text (its String()); none for null, floats, containers
+                int32_t ta = 0;
+                uint32_t tn = 0xFFFFFFFFu;
+                const int32_t ra = roff + (int32_t)vpos;
+                if (type == T_STRING && !open && !esc) {
+                    ta = ra + 1;
+                    tn = end - vpos - 2u;
+                } else if (type == T_NUMBER && !open) {  // literals must be exact (gjson takes any letters)
                     const uint32_t b0 = ring[ra];
+                    const uint32_t n = end - vpos;
+                    const uint64_t w = ring64(ring, ra);
+                    for (uint32_t k = 0; k < n; k += 4u) {  // (gjson's scalar ends at a byte <= ' ')
+                        const uint32_t q = ring32(ring, ra + (int32_t)k);
+                        const uint32_t m = n - k >= 4 ? ~0u : (1u << (8u * (n - k))) - 1u;
+                        if (le20_bytes(q) & m) {
+                            bad |= 1u << i;
+                            break;
+                        }
+                    }
                     if (b0 == 't' || b0 == 'f' || b0 == 'n') {
-                        const uint64_t w = ring64(ring, ra);
-                        const uint32_t n = end - vpos;
                         if (b0 == 't' && n == 4 && (uint32_t)w == 0x65757274u) type = T_TRUE;
                         else if (b0 == 'f' && n == 5 && (w & 0xFFFFFFFFFFull) == 0x65736C6166ull) type = T_FALSE;
                         else if (b0 == 'n' && n == 4 && (uint32_t)w == 0x6C6C756Eu) type = T_NULL;
                         else bad |= 1u << i;  // (left to the exact scan)
+                        if (type == T_TRUE || type == T_FALSE) ta = ra, tn = n;
+                    } else if (n <= 16) {  // -?[0-9]+ is its own String()
+                        const uint64_t w1 = ring64(ring, ra + 8);
+                        const uint32_t k0 = b0 == '-' ? 1u : 0u;
+                        const uint64_t m0 = n >= 8 ? ~0ull : (1ull << (8 * n)) - 1ull;
+                        const uint64_t m1 = n >= 16 ? ~0ull : n > 8 ? (1ull << (8 * (n - 8))) - 1ull : 0ull;
+                        const uint64_t d0 = w ^ 0x3030303030303030ull, d1 = w1 ^ 0x3030303030303030ull;
+                        const uint64_t nd0 = ((d0 + 0x7676767676767676ull) | d0) & 0x8080808080808080ull &
+                                             m0 & ~(k0 ? 0xFFull : 0ull);
+                        const uint64_t nd1 = ((d1 + 0x7676767676767676ull) | d1) & 0x8080808080808080ull & m1;
+                        if (!nd0 && !nd1 && n > k0) ta = ra, tn = n;
                     }
                 }
                 // first match in document order: a second one sends the document to the exact scan
@@ -719,16 +826,13 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                     bad |= 1u << i;
                     continue;
                 }
-#if !defined(__HIPCC__) && defined(AJX_STREAM_DEBUG)
-                std::fprintf(stderr, "cap t%u l%u doc%u sel%u vpos%u type%u open%u end%u\n", t, l, doc, s, vpos, type, open, end);
-#endif
-                const uint32_t meta = open ? (kOpenEnd | (kTypeUnknown << 24))
+                const uint32_t meta = open ? (kOpenEnd | (kTypeUnknown << 24) | (arr << 29))
                                            : (((end - vpos) & 0xFFFFFFu) | (type << 24) | (esc << 27));
                 reinterpret_cast<uint32_t*>(&row[1u + s])[1] = meta;
-                // eager patterns on a string's text
-                if (T.eg && type == T_STRING && !open && !esc) {
+                // eager patterns on the value's text
+                if (T.eg && tn != 0xFFFFFFFFu) {
                     const EagerSel eg = T.eg[s];
-                    const uint32_t hit = eager_hits(eg, ring, roff + (int32_t)vpos + 1, end - vpos - 2u);
+                    const uint32_t hit = eager_hits(eg, ring, ta, tn);
                     uint64_t dD = 0, dT = 0;
 #pragma unroll
                     for (int k = 0; k < 2; k++) {
@@ -738,9 +842,6 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                         dD |= bit;
                         if (((hit >> k) & 1u) == (op == OP_EQ || op == OP_INCL ? 1u : 0u)) dT |= bit;
                     }
-#if !defined(__HIPCC__) && defined(AJX_STREAM_DEBUG)
-                    std::fprintf(stderr, "eager doc%u sel%u hit%u dD %llx dT %llx bytes %016llx\n", doc, s, hit, (unsigned long long)dD, (unsigned long long)dT, (unsigned long long)ring64(ring, roff + (int32_t)vpos + 1));
-#endif
                     if (dD) {
                         wave::lds_or64(&dec[0], dD);
                         if (dT) wave::lds_or64(&dec[1], dT);
@@ -786,7 +887,10 @@ AJX_HD bool resolve_open(const uint8_t* d, uint32_t n, uint32_t a, uint64_t* rec
         }
     } else {
         type = T_NUMBER;
-        while (end < n && d[end] != ',' && d[end] != '}' && d[end] != ']') end++;
+        while (end < n && d[end] != ',' && d[end] != '}' && d[end] != ']') {
+            if (d[end] <= ' ') return false;  // (gjson's scalar would end there)
+            end++;
+        }
         const uint32_t k = end - a;
         if (b0 == 't' || b0 == 'f' || b0 == 'n') {  // literals must be exact (as the stream's)
             const bool t = b0 == 't' && k == 4 && d[a + 1] == 'r' && d[a + 2] == 'u' && d[a + 3] == 'e';
@@ -801,27 +905,98 @@ AJX_HD bool resolve_open(const uint8_t* d, uint32_t n, uint32_t a, uint64_t* rec
     return true;
 }
 
-// Stage B for request r (document d, n bytes) on its capture row in LDS: the open values,
-// the found bits, then ajx_fast.h's patterns_from_row, the T bitmap and the fold of every
-// tree. false: the request needs the exact scan (the caller puts it on the slow list).
-AJX_HD bool finish(uint32_t r, const uint8_t* blob, const uint8_t* d, uint32_t n, uint64_t* row, uint32_t ns,
-                   const uint64_t dec[2], uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-                   uint64_t* __restrict__ out_bm, uint32_t stride) {
-    uint64_t found = 0;
-    for (uint32_t s = 0; s < ns; s++) {
-        uint64_t rec = row[1u + s];
-        if ((uint32_t)rec == kNone) continue;
-        found |= 1ull << s;
-        if ((rec >> 32) & kOpenEnd) {
-            if (!resolve_open(d, n, (uint32_t)rec, &rec)) return false;
-            row[1u + s] = rec;
+// The arrays the stream compared element by element decide their selectors' incl / excl
+// patterns: dD / dT (decided, true) from the eager words dw and the row's records.
+AJX_HD void array_decisions(const EagerSel* eg, uint32_t ns, RowRef row, const uint64_t dw[4], uint64_t& dD,
+                            uint64_t& dT) {
+    if (!eg) return;
+    for (uint32_t s = 0; s < ns && s < 32u; s++) {
+        const uint64_t rec = row[1u + s];
+        const uint32_t meta = (uint32_t)(rec >> 32);
+        if ((uint32_t)rec == kNone || !(meta & kOpenEnd) || !((meta >> 29) & 1u) || ((dw[3] >> s) & 1ull)) continue;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t em = eg[s].m[k], op = (em >> 8) & 0xFFu;
+            if (!(em & kEagerValid) || (op != OP_INCL && op != OP_EXCL)) continue;
+            const uint64_t bit = 1ull << (em & 63u);
+            dD |= bit;
+            if (((dw[2] >> (2u * s + (uint32_t)k)) & 1ull) == (op == OP_INCL ? 1ull : 0ull)) dT |= bit;
         }
     }
-    row[0] = found;
+}
+
+// Folds request r when the stream decided every one of its patterns (eager patterns, arrays
+// compared element by element, selectors not found): the T bitmap and every tree's
+// result. false: some pattern needs stage B (ajx_stream_finish).
+AJX_HD bool finish_light(uint32_t r, const uint8_t* blob, const Tabs& T, const uint64_t* row, const uint64_t dw[4],
+                         uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
+                         uint32_t stride) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    const uint32_t np = h->n_patterns;
+    if (np > 64 || (h->static_error[0] | h->unsupported[0])) return false;
+    uint64_t dD = dw[0], dT = dw[1];
+    array_decisions(T.eg, T.ns, RowRef(row), dw, dD, dT);
+    const SelectorPatterns* sps = reinterpret_cast<const SelectorPatterns*>(blob + h->off_sel_patterns);
+    uint64_t t0 = dT & dD, all = dD;
+    for (uint32_t s = 0; s < T.ns; s++)
+        if ((uint32_t)row[1u + s] == kNone) {  // Null: the compiler's null_true bits
+            t0 |= sps[s].mask[0] & h->null_true[0];
+            all |= sps[s].mask[0];
+        }
+    const uint64_t want = np >= 64 ? ~0ull : (1ull << np) - 1ull;
+    if ((all & want) != want) return false;
+    const uint64_t t[2] = {t0 & want, 0ull}, u[2] = {0ull, 0ull}, se[2] = {0ull, 0ull};
+    if (out_bm) {
+        uint64_t* orow = out_bm + (size_t)r * stride;
+        orow[0] = t[0];
+        for (uint32_t w = 1; w < stride; w++) orow[w] = 0ull;
+    }
+    const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
+    const uint32_t nt = h->pad1[0];
+    if (nt == 0) {
+        int32_t ep;
+        out_tri[r] = run_fold_bits(code, h->n_code, t, u, se, &ep);
+        if (out_err) out_err[r] = ep;
+        return true;
+    }
+    const uint32_t* rc = reinterpret_cast<const uint32_t*>(blob + h->pad1[1]);
+    for (uint32_t k = 0; k < nt; k++) {
+        int32_t ep;
+        out_tri[(size_t)r * nt + k] = run_fold_bits(code + rc[2 * k], rc[2 * k + 1], t, u, se, &ep);
+        if (out_err) out_err[(size_t)r * nt + k] = ep;
+    }
+    return true;
+}
+
+// Stage B for a request the stream did not decide (ajx_stream_finish, one work-item per
+// request; its row in HBM: found word, records, the 4 eager words): the open values from
+// the document, the arrays' decisions, ajx_fast.h's patterns_from_row, the T bitmap and the
+// fold. false: the exact scan decides the request (the row is marked kRowSlow).
+AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint32_t n, RowRef row,
+                        uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
+                        uint32_t stride) {
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
+    const uint32_t ns = h->n_selectors;
+    const EagerSel* eg = h->off_eager ? reinterpret_cast<const EagerSel*>(blob + h->off_eager) : nullptr;
+    const uint64_t dw[4] = {row[1u + ns], row[2u + ns], row[3u + ns], row[4u + ns]};
+    uint64_t dD = dw[0], dT = dw[1];
+    array_decisions(eg, ns, row, dw, dD, dT);
+    for (uint32_t s = 0; s < ns; s++) {
+        uint64_t rec = row[1u + s];
+        if ((uint32_t)rec == kNone || !((rec >> 32) & kOpenEnd)) continue;
+        if (!resolve_open(d, n, (uint32_t)rec, &rec)) {
+            row[0] = kRowSlow;
+            return false;
+        }
+        row[1u + s] = rec;
+    }
     uint64_t t[2], u[2];
-    patterns_from_row(blob, d, RowRef(row), t, u, dec);
-    if ((u[0] & ~h->unsupported[0]) | (u[1] & ~h->unsupported[1])) return false;
+    const uint64_t dec[2] = {dD, dT};
+    patterns_from_row(blob, d, row, t, u, dec);
+    if ((u[0] & ~h->unsupported[0]) | (u[1] & ~h->unsupported[1])) {
+        row[0] = kRowSlow;
+        return false;
+    }
     if (out_bm) {
         uint64_t* orow = out_bm + (size_t)r * stride;
         orow[0] = t[0];
@@ -846,15 +1021,18 @@ AJX_HD bool finish(uint32_t r, const uint8_t* blob, const uint8_t* d, uint32_t n
     return true;
 }
 
-// The whole span for this lane: setup, the steps, then stage B for request span * kSpan + l.
-// `rows`: the wave's capture rows (LDS, lds_bytes). Returns false when request r (if it
-// exists) needs the exact scan; rows_out (optional): the row copied out for
-// select_from_eval.
+enum : uint32_t { R_DONE = 0, R_SLOW = 1, R_STAGE_B = 2 };
+
+// The whole span for this lane: setup, the steps, then request r = span * kSpan + l
+// (l < kSpan): R_DONE (decided and folded; its row holds captures with possibly open
+// ends), R_SLOW (the exact scan decides it) or R_STAGE_B (its row and eager words, *row_out
+// / *dw_out, go to finish_full).
 template <int MODE = 0>
-AJX_HD bool scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const uint8_t* __restrict__ arena,
-                      const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n, uint32_t span,
-                      uint32_t l, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-                      uint64_t* __restrict__ out_bm, uint32_t stride) {
+AJX_HD uint32_t scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const uint8_t* __restrict__ arena,
+                          const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
+                          uint32_t span, uint32_t l, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                          uint64_t* __restrict__ out_bm, uint32_t stride, const uint64_t** row_out,
+                          const uint64_t** dw_out) {
     const Tabs T = tabs_of(blob);
     const uint32_t r = span * kSpan + l;
     const bool my = l < kSpan && r < n;
@@ -871,7 +1049,7 @@ AJX_HD bool scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const uin
     fetch(L, arena, 0, total, l, my_start, my, kNone, cur, Hc);
     uint32_t last_doc = kNone + (uint32_t)__builtin_popcountll(Hc);
     for (uint32_t t = 0; t < nsteps; t++) {
-        Blk nxt;
+        Blk nxt{};
         uint64_t Hn = 0;
         if (t + 1u < nsteps) fetch(L, arena, t + 1u, total, l, my_start, my, last_doc, nxt, Hn);
         step<MODE>(L, rows, T, t, l, cur, Hc, c);
@@ -880,21 +1058,27 @@ AJX_HD bool scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const uin
         last_doc += (uint32_t)__builtin_popcountll(Hn);
     }
     wave::sync();
-    if (!my) return true;
+    if (!my) return R_DONE;
     if constexpr (MODE == 1) {
         out_tri[r] = (uint8_t)(L.bad[l] > L.root_end[l]);
-        return true;
+        return R_DONE;
     }
     const bool proved = L.root_end[l] != kNone && L.bad[l] > L.root_end[l];
-    if (!proved) return false;
+    if (!proved) return R_SLOW;
     uint64_t* row = rows + (size_t)l * (1u + T.ns);
-    const uint64_t* dw = rows + (size_t)kSpan * (1u + T.ns) + 2u * l;
-    const uint64_t dec[2] = {dw[0], dw[1]};
+    const uint64_t* dp = rows + (size_t)kSpan * (1u + T.ns) + 4u * l;
+    *row_out = row;
+    *dw_out = dp;
+    uint64_t found = 0;
+    for (uint32_t s = 0; s < T.ns; s++)
+        if ((uint32_t)row[1u + s] != kNone) found |= 1ull << s;
+    row[0] = found;
     if constexpr (MODE == 2) {  // (profiling: no stage B)
-        out_tri[r] = (uint8_t)(row[1] ^ dec[0] ^ dec[1]);
-        return true;
+        out_tri[r] = (uint8_t)(row[1] ^ dp[0] ^ dp[1] ^ dp[2]);
+        return R_DONE;
     }
-    return finish(r, blob, arena + off, len, row, T.ns, dec, out_tri, out_err, out_bm, stride);
+    const uint64_t dw[4] = {dp[0], dp[1], dp[2], dp[3]};
+    return finish_light(r, blob, T, row, dw, out_tri, out_err, out_bm, stride) ? R_DONE : R_STAGE_B;
 }
 
 }  // namespace stream

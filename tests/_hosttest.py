@@ -235,9 +235,9 @@ def json_valid(text) -> int:
 
 
 def eval_stream(hr, arena, offs, lens, mode=0, stride=2, dbg=None):
-    """The streaming scan (ajx_stream.h) over a batch on the host emulation of the wave:
-    (tri, err, bitmap, slow) — slow[r] = 1 where it hands request r to the exact scan; None
-    when the ruleset has no stream tables."""
+    """The streaming scan (ajx_stream.h) over a batch on the host emulation of the wave,
+    then its stage B: (tri, err, bitmap, slow) — slow[r] = 1 where request r goes to the
+    exact scan, 2 where stage B decided it; None when the ruleset has no stream tables."""
     L = lib()
     if not getattr(L, "_stream_decl", False):
         L.ht_eval_stream.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,

@@ -313,10 +313,10 @@ extern "C" void ht_lean_counts(uint64_t* iters, uint64_t* subs) {
 // ---- the streaming scan (ajx_stream.h) on 64 host threads per wave (ajx_wave.h) ----
 #include "../../authorino_amd/csrc/ajx_stream.h"
 
-// every request of the batch through the stream kernel's code, one span (wave) at a time;
-// out_slow[r] = 1 where the stream hands the request to the exact scan (outputs unset).
-// mode 1: structure only (out_tri[r] = proved). Returns -1 when the ruleset has no stream
-// tables.
+// every request of the batch through the stream kernel's code, one span (wave) at a time,
+// then stage B (finish_full) for those it hands over; out_slow[r] = 1 where the exact scan
+// decides request r (outputs unset), 2 where stage B decided it. mode 1: structure only
+// (out_tri[r] = proved). Returns -1 when the ruleset has no stream tables.
 extern "C" int ht_eval_stream(void* h, const uint8_t* arena, const uint64_t* offs, const uint32_t* lens, uint32_t n,
                               uint8_t* out_tri, int32_t* out_err, uint64_t* out_bm, uint32_t stride, uint8_t* out_slow,
                               int mode, uint32_t* out_dbg) {
@@ -330,23 +330,42 @@ extern "C" int ht_eval_stream(void* h, const uint8_t* arena, const uint64_t* off
     const uint32_t ns = hd->n_selectors;
     const uint32_t spans = (n + stream::kSpan - 1) / stream::kSpan;
     std::vector<uint64_t> wl(stream::lds_bytes(ns) / 8 + 2);
+    std::vector<uint64_t> stage_rows((size_t)n * (5 + ns));
+    std::vector<uint32_t> stage_list;
     for (uint32_t span = 0; span < spans; span++) {
         std::memset(wl.data(), 0xA5, wl.size() * 8);
         stream::WaveLds& L = *reinterpret_cast<stream::WaveLds*>(wl.data());
         uint64_t* rows = wl.data() + sizeof(stream::WaveLds) / 8;
+        std::mutex mu;
         wave::run_wave([&](uint32_t l) {
-            bool ok;
+            const uint64_t *rowp = nullptr, *dwp = nullptr;
+            uint32_t res;
             if (mode == 1)
-                ok = stream::scan_span<1>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm, stride);
+                res = stream::scan_span<1>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm,
+                                           stride, &rowp, &dwp);
             else
-                ok = stream::scan_span<0>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm, stride);
+                res = stream::scan_span<0>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm,
+                                           stride, &rowp, &dwp);
             const uint32_t r = span * stream::kSpan + l;
-            if (l < stream::kSpan && r < n) out_slow[r] = ok ? 0 : 1;
-            if (l < stream::kSpan && r < n && out_dbg) {  // (bad position, root close)
+            if (l >= stream::kSpan || r >= n) return;
+            out_slow[r] = res == stream::R_SLOW ? 1 : 0;
+            if (res == stream::R_STAGE_B) {
+                uint64_t* o = stage_rows.data() + (size_t)r * (5 + ns);
+                std::memcpy(o, rowp, (1 + ns) * 8);
+                std::memcpy(o + 1 + ns, dwp, 4 * 8);
+                std::lock_guard<std::mutex> g(mu);
+                stage_list.push_back(r);
+            }
+            if (out_dbg) {  // (bad position, root close)
                 out_dbg[2 * r] = L.bad[l];
                 out_dbg[2 * r + 1] = L.root_end[l];
             }
         });
+    }
+    for (uint32_t r : stage_list) {
+        RowRef row(stage_rows.data() + (size_t)r * (5 + ns));
+        const bool ok = stream::finish_full(r, blob, arena + offs[r], lens[r], row, out_tri, out_err, out_bm, stride);
+        out_slow[r] = ok ? 2 : 1;
     }
     return 0;
 }
