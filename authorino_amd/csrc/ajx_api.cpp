@@ -88,9 +88,8 @@ struct authjx_ctx {
     int no_tenant_stage = 0;  // profiling: multi-tenant batches read tables from global memory
     int force_scan = 0;
     int ablate = 0;  // profiling / comparison only: 41 the lean single-pass kernel where the
-                     // streaming kernel would run, 40 the token-scanner single-pass kernel,
-                     // 50 / 51 the streaming kernel's structural pass alone / without its
-                     // fold, 1..3 / 10..12
+                     // streaming kernel would run, 50 / 51 the streaming kernel's
+                     // structural pass alone / without its fold, 1..3 / 10..12
                      // token-scanner ablations and workgroup sizes
 };
 
@@ -440,15 +439,15 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     }
     HIP_OK(hipEventRecord(w->ev0, s));
     // kernel: the streaming kernel (ajx_stream.h) for a one-ruleset batch whose ruleset it
-    // takes, else the lean single-pass kernel (ajx_lean.h; ablate 40: the token scanner of
-    // ajx_fast.h) or the multi-tenant kernel; the exact scan for what they hand over
+    // takes, else the lean single-pass kernel (ajx_lean.h) or the multi-tenant kernel; the
+    // exact scan for what they hand over
     bool mods = false;  // modifier chains: the exact scan's instance with text buffers
     for (uint32_t i = 0; i < n_sets; i++)
         mods = mods || reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->n_modifiers != 0 ||
                (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagBufs) != 0;
     // capture rows kept for authjx_select_from_eval_device: one forest ruleset
     // (authjx_compile_forest), a full kernel
-    const bool full = ablate == 0 || ablate == 40 || ablate == 41 || (ablate >= 10 && ablate <= 12);
+    const bool full = ablate == 0 || ablate == 41 || (ablate >= 10 && ablate <= 12);
     const auto* h0 = reinterpret_cast<const ajx::RulesetHdr*>(sets[0]->c.blob.data());
     const bool keep_rows = !force_scan && n_sets == 1 && full && h0->pad1[0] != 0;
     w->rows_rs = keep_rows ? sets[0] : nullptr;
@@ -486,7 +485,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                      d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
                                      w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
-                                     (ablate < 20 || ablate == 40) ? ablate : 0, perm, mods));
+                                     ablate < 20 ? ablate : 0, perm, mods));
     }
     return batch_done(w, sets, n_sets);
 }

@@ -337,10 +337,9 @@ __global__ __launch_bounds__(kFastMaxBlock) void ajx_patterns(const uint8_t* con
     (void)finish_request(r, blob, arena + offs[r], row, out_tri, out_err, out_bm, stride);  // (profiling split)
 }
 
-// The single-pass path: stage A then stage B in the same work-item, while the
-// request's value bytes are still in cache (a separate stage-B launch re-reads them
-// from HBM). Requests stage A can not prove gjson-equivalent go to the slow list.
-template <bool SHARED>
+// The token-scanner single-pass kernel for multi-tenant batches without staging: stage A
+// then stage B in the same work-item, every table read from global memory through the
+// request's own ruleset. Requests stage A can not prove gjson-equivalent go to the slow list.
 __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(const uint8_t* const* __restrict__ sets,
                                                       const uint32_t* __restrict__ set_of_req,
                                                       const uint8_t* __restrict__ arena,
@@ -356,7 +355,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
     // its capture row is row k of the wave-interleaved layout (wave_row)
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t r = k < n ? (perm ? perm[k] : k) : 0u;
-    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : set_of_req[r]]);
+    const uint8_t* blob = sets[set_of_req ? set_of_req[r] : 0];
     if (k >= n) return;
     const RowRef row = wave_row(rows, row_stride, k);
     const uint8_t* d = arena + offs[r];
@@ -364,24 +363,10 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
-#ifdef AJX_ABLATE_FUSED_NOB  // profiling: stage A alone (outputs meaningless)
-    out_tri[r] = (uint8_t)row[0];
-    return;
-#endif
     if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
         row[0] = kRowSlow;
         slow_ids[atomicAdd(slow_count, 1u)] = r;
     }
-}
-
-// stage B of the lean kernel as a call (not inlined): the scan's live state ends before it,
-// so the two stages do not share one register allocation
-__device__ __attribute__((noinline)) bool lean_finish(uint32_t r, const uint8_t* blob, const uint8_t* d, RowRef row,
-                                                      uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-                                                      uint64_t* __restrict__ out_bm, uint32_t stride, uint64_t dec0,
-                                                      uint64_t dec1) {
-    const uint64_t dec[2] = {dec0, dec1};
-    return finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec);
 }
 
 // The lean single-pass kernel (ajx_lean.h): stage A with the lean scan, then stage B in the
@@ -423,15 +408,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_lean(
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
-#ifdef AJX_ABLATE_FUSED_NOB  // profiling: stage A alone (outputs meaningless)
-    out_tri[r] = (uint8_t)row[0];
-    return;
-#endif
-#ifdef AJX_LEAN_CALL_B  // (profiling: stage B as a call; measured slower: c2 1.54 vs 1.52 ms, c5 16.2 vs 14.6)
-    if (!lean_finish(r, blob, d, row, out_tri, out_err, out_bm, stride, dec[0], dec[1])) {
-#else
     if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec)) {
-#endif
         row[0] = kRowSlow;
         slow_ids[atomicAdd(slow_count, 1u)] = r;
     }
@@ -957,8 +934,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             reinterpret_cast<const void*>(&ajx_scan_fast<0, false>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<1, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<2, true>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused<true>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused<false>),
+                            reinterpret_cast<const void*>(&ajx_scan_fused),
                             reinterpret_cast<const void*>(&ajx_scan_lean<true>),
                             reinterpret_cast<const void*>(&ajx_scan_lean<false>)};
         for (const void* k : ks) {
@@ -999,7 +975,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
             hipLaunchKernelGGL((ajx_patterns<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
         }
-    } else if (mode != 40 && !(d_set_of_req && !shared)) {  // the lean single-pass kernel (default)
+    } else if (!d_set_of_req) {  // the lean single-pass kernel (one ruleset)
         // (multi-tenant batches: the staged tenant scanner below. Measured on c4, the lean
         // scan with per-lane table parameters took 6.39 ms and one pass per ruleset of a
         // wave 7.3-7.8 ms, against 5.38 ms for the tenant kernel's LDS-staged tables)
@@ -1014,11 +990,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
             hipLaunchKernelGGL((ajx_scan_lean<false>), dim3(lgrid), dim3(lblock), llds, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
                                d_bm, stride, ring_off, d_perm);
-    } else if (shared) {  // the token-scanner single-pass kernel (kernel mode 40)
-        hipLaunchKernelGGL((ajx_scan_fused<true>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena,
-                           d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride,
-                           ring_off, d_perm);
-    } else if (d_set_of_req && shared_blob_bytes) {
+    } else if (shared_blob_bytes) {
         // multi-tenant batch (shared_blob_bytes != 0: staging on): each workgroup stages its
         // runs' rulesets, those that fit (ajx_scan_fused_tenant);
         // 4-wave workgroups, so more of them fall inside one AuthConfig's bucket
@@ -1030,7 +1002,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                            stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count,
                            d_slow_ids, d_tri, d_err, d_bm, stride, toff, d_perm);
     } else {
-        hipLaunchKernelGGL((ajx_scan_fused<false>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
+        hipLaunchKernelGGL(ajx_scan_fused, dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
                            d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,
                            stride, ring_off, d_perm);
     }

@@ -41,6 +41,7 @@ def lib():
         L.ht_select_value.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                       C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ht_select_value.restype = C.c_int
+        L.ht_inject_truncate.argtypes = [C.c_int]
         L.ht_json_valid.argtypes = [C.c_char_p, C.c_uint32]
         L.ht_json_valid.restype = C.c_int
         L.ht_string.restype = C.c_int

@@ -77,6 +77,11 @@ int ht_eval(void* h, const uint8_t* doc_in, uint32_t len, uint8_t* res, int32_t*
     return run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
 }
 
+// fault injection for the checker tests (tests/test_checker_sensitivity.py): 1 drops the
+// last byte of every built text value select_value returns, as a kernel bug would
+static int g_inject_truncate = 0;
+void ht_inject_truncate(int on) { g_inject_truncate = on; }
+
 // select_value (ajx_modifiers.h): the value of pattern p's selector as the select kernel
 // resolves it with a text slot; returns 0, or -1 undecided (out = {start, len, type | esc << 8})
 int ht_select_value(void* h, uint32_t p, const uint8_t* doc_in, uint32_t len, uint8_t* text, uint32_t cap,
@@ -89,7 +94,9 @@ int ht_select_value(void* h, uint32_t p, const uint8_t* doc_in, uint32_t len, ui
     const Selector* sels = (const Selector*)(blob + hd->off_selectors);
     const Pattern* pats = (const Pattern*)(blob + hd->off_patterns);
     static ModBufs mb;
-    return select_value(blob, sels[pats[p].selector], doc, len, mb, text, cap, used, out) ? 0 : -1;
+    if (!select_value(blob, sels[pats[p].selector], doc, len, mb, text, cap, used, out)) return -1;
+    if (g_inject_truncate && ((out[2] >> 8) & kValText) && out[1]) out[1]--;
+    return 0;
 }
 
 // json_valid (ajx_modifiers.h, gjson Valid): 1 valid, 0 invalid, -1 undecided (depth)

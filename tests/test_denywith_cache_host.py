@@ -64,20 +64,20 @@ def test_modifier_value_selectors_resolve_to_built_text():
     """denyWith / cache-key selectors with the reference's modifiers and "#." lists
     (json.go:96-151, :161-264): their values are the modifier chain's Result (built text
     in the request's select text slot, AUTHJX_VALUE_TEXT), never the unmodified value; a
-    value the device cannot build (@case on a SpecialCasing character) leaves that request
-    undecided."""
+    value the oracle stand-in cannot build (@case on non-ASCII text: it restates ASCII only)
+    leaves that request undecided (the device decides it: tests/test_gpu_select_text.py)."""
     dw = P.DenyWithValues(message=JSONValue(pattern="auth.identity.tenant.@case:upper"),
                           body=JSONValue(pattern='{auth.identity.sub|@extract:{"sep":"i","pos":0}}-{auth.identity.roles.#.x}'),
                           headers=[("X-Roles", JSONValue(pattern="auth.identity.roles|@case:upper"))])
     cfg = P.AuthConfig(authorization=[_deny_all()], unauthorized=dw)
-    # (ß upper-cases to "SS" under SpecialCasing: a mapping the device tables leave undecided)
+    # (non-ASCII under @case: the oracle stand-in leaves it undecided)
     raw_tenant = _req(sub="bob", tenant="zeta").replace(b'"zeta"', '"straße"'.encode())
     res = P.AuthPipelineBatch(cfg, ctx=OracleCtx()).evaluate([_req(), raw_tenant])
     r = res[0]
     assert not r.undecided and r.code == P.CODE_PERMISSION_DENIED
     assert r.message == "ACME" and r.body == "al-[]"
     assert r.deny_headers == [{"X-Roles": '["USER"]'}]
-    assert res[1].undecided and res[1].code == P.CODE_UNKNOWN  # (special casing)
+    assert res[1].undecided and res[1].code == P.CODE_UNKNOWN  # (the oracle: ASCII only)
     # a cache key through a modifier: requests with the same key after @case:lower share
     # the cached decision (authorization.go:59-74)
     cached = P.AuthorizationConfig(

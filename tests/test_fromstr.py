@@ -129,7 +129,7 @@ def test_fromstr_and_tails_match_oracle(seed):
     malformed / scalar bodies, non-string inputs, missing keys."""
     rng = random.Random(4200 + seed)
     hrs = {}
-    checked = undecided = 0
+    checked = 0
     for _ in range(400):
         d = _fromstr_doc(rng)
         for p in PATHS:
@@ -141,9 +141,7 @@ def test_fromstr_and_tails_match_oracle(seed):
                 hrs[p] = H.HostRuleset([(p, 1, "")], [(0, -1, -1, 0)], 0)
                 assert hrs[p].status == [0], p
             rc, out, _ = hrs[p].select_value(0, d, text := bytearray(8192), 0)
-            if rc != 0:
-                undecided += 1
-                continue
+            assert rc == 0, ("undecided", d, p)  # (no reason to leave one undecided here)
             st, ln, tt = out
             src = bytes(text) if (tt >> 8) & 4 else d
             assert (tt & 0xFF, src[st:st + ln]) == want, (d, p)
@@ -152,7 +150,7 @@ def test_fromstr_and_tails_match_oracle(seed):
             _, _, res = hr.eval(d)
             assert res == [1, 0], (d, p, want_s)
             checked += 1
-    assert checked > 2500 and undecided <= checked // 20, (checked, undecided)
+    assert checked > 2500, checked
 
 
 def test_reference_jwt_chain():

@@ -4,6 +4,7 @@ modifiers and "#." lists as VALUES — response headers, denyWith and evaluator-
 pkg/service/auth_pipeline.go:581-608). The select kernel's TEXT instance builds each
 such value (authjx_select_text_batch[_device]) into the request's text slot; the bytes
 and types are compared with the oracle's gjson.Get with the same modifiers."""
+import collections
 import json
 import random
 
@@ -35,6 +36,24 @@ def _check(vals, text, k, j, d, want):
     src = text[k].tobytes() if (tt >> 8) & 4 else d
     t, raw = want
     assert (tt & 0xFF, src[st:st + ln]) == (t, raw), (d[:200], k, j)
+    return ln if (tt >> 8) & 4 else 0
+
+
+def _check_request(vals, text, k, d, wants, stride, counts):
+    """Request k's values in slot order: each equals the oracle's, or is UNDECIDED (255)
+    for the one reason the select kernel has on these inputs — its built text does not
+    fit what is left of the request's text slot (`stride` bytes). counts: tallies."""
+    used = 0
+    for j, want in enumerate(wants):
+        if want is None:  # (the oracle restates @case / @strip for ASCII text only:
+            counts["skipped"] += 1  # tests/test_unicode_case.py pins the Unicode tables)
+            continue
+        if (int(vals[k, j, 2]) & 0xFF) == 255:
+            assert used + len(want[1]) > stride, ("undecided without a reason", d[:200], k, j, want)
+            counts["undecided: text slot full"] += 1
+            continue
+        used += _check(vals, text, k, j, d, want)
+        counts["checked"] += 1
 
 
 def test_modifier_chains_as_values_match_oracle(ctx):
@@ -158,10 +177,12 @@ def test_denywith_and_cache_keys_with_modifiers_on_device(ctx):
     docs = [_req(sub="s%d" % i, tenant="t%d" % (i % 7), roles=("r%d" % i, "x")) for i in range(300)]
     docs.append(_req(sub="bob", tenant="zeta").replace(b'"zeta"', '"straße"'.encode()))  # (SpecialCasing)
     got = P.AuthPipelineBatch(cfg(), ctx=ctx).evaluate(docs)
-    want = P.AuthPipelineBatch(cfg(), ctx=OracleCtx()).evaluate(docs)
+    want = P.AuthPipelineBatch(cfg(), ctx=OracleCtx()).evaluate(docs[:-1])
     key = lambda r: (r.code, r.undecided, r.message, r.body, r.deny_headers, r.status)  # noqa: E731
-    assert [key(r) for r in got] == [key(r) for r in want]
-    assert got[0].message == "T0" and got[-1].undecided
+    assert [key(r) for r in got[:-1]] == [key(r) for r in want]
+    assert got[0].message == "T0"
+    # (the oracle restates @case for ASCII only; Go's strings.ToUpper keeps ß: simple mapping)
+    assert not got[-1].undecided and got[-1].message == "STRAßE", key(got[-1])
     cache_cfg = lambda: P.AuthorizationConfig(  # noqa: E731
         "c", rules=J.All(J.Pattern("auth.identity.sub", J.EqualOperator, "alice")),
         cache=CA.EvaluatorCache(JSONValue(pattern="{auth.identity.tenant|@case:lower}/{auth.identity.sub}"), 60))
@@ -184,18 +205,11 @@ def test_fromstr_and_tails_on_device(ctx):
     rs = ctx.compile([(p, 1, "") for p in PATHS], [], -1)
     assert rs.status == [0] * len(PATHS)
     vals, text = ctx.select_text_host_arena([rs], arena, offs, lens, text_stride=8192)
-    checked = und = 0
+    counts = collections.Counter()
     for k, d in enumerate(docs):
-        for j, p in enumerate(PATHS):
-            want = O.gjson_get_mods(d, p)
-            if want is None:  # (non-ASCII under @case: not restated by the oracle)
-                continue
-            if (int(vals[k, j, 2]) & 0xFF) == 255:
-                und += 1
-                continue
-            _check(vals, text, k, j, d, want)
-            checked += 1
-    assert checked > 25000 and und <= checked // 20, (checked, und)
+        _check_request(vals, text, k, d, [O.gjson_get_mods(d, p) for p in PATHS], 8192, counts)
+    print(dict(counts))
+    assert counts["checked"] > 25000, counts
     jwt = 'access_token.@extract:{"pos":1}|@extract:{"sep":".","pos":1}|@base64:decode|@fromstr'
     pats = [(PATHS[1], 1, "authorino"), (PATHS[1], 2, "authorino"), (PATHS[3], 1, "AdmissionReview"),
             (PATHS[2], 3, "AdmissionReview"), (PATHS[0], 1, ""), (PATHS[7], 1, "5"), (PATHS[9], 1, "v"),
@@ -210,9 +224,10 @@ def test_fromstr_and_tails_on_device(ctx):
     orc = O.Ruleset(pats, nodes, root)
     tri, _, bm = ctx.eval_host_arena([dev], arena, offs, lens)
     otri, _, obm = O.eval_batch([orc], arena, offs, lens, nthreads=8)
-    ok = (tri != runtime.UNDECIDED) & (otri != runtime.UNDECIDED)
-    assert ok.sum() >= 0.9 * len(docs)
-    assert np.array_equal(tri[ok], otri[ok]) and np.array_equal(bm[ok], obm[ok])
+    # (every request decided by both, identically: the host build of the same code decides
+    # all of them, tests/test_fromstr.py)
+    print({"undecided": int((tri == runtime.UNDECIDED).sum()), "oracle undecided": int((otri == runtime.UNDECIDED).sum())})
+    assert np.array_equal(tri, otri) and np.array_equal(bm, obm)
     assert (bm[-1, 0] >> 8) & 1 and (bm[-1, 0] >> 9) & 1  # (the JWT claims)
 
 
@@ -220,28 +235,42 @@ def test_unicode_case_and_strip_on_device(ctx):
     """@case / @strip on non-ASCII and invalid UTF-8 text through the kernels (the Unicode
     tables of ajx_unicode.h in device memory) against tests/test_unicode_case.py's Go
     restatement; SpecialCasing / unassigned code points UNDECIDED (255)."""
-    from test_unicode_case import Undecided, _raw_string, go_case, go_strip
+    from test_unicode_case import _raw_string
 
     rng = random.Random(6200)
     raws = [_raw_string(rng) for _ in range(3000)]
     docs = [b'{"s":' + r + b',"n":1}' for r in raws]
-    paths = ["s.@case:upper", "s|@case:lower", "s.@strip"]
-    fns = [lambda r: go_case(r, True), lambda r: go_case(r, False), go_strip]
-    rs = ctx.compile([(p, 1, "") for p in paths], [], -1)
+    rs = ctx.compile([(p, 1, "") for p in UNICODE_PATHS], [], -1)
     arena, offs, lens = _pack(docs)
     vals, text = ctx.select_text_host_arena([rs], arena, offs, lens, text_stride=2048)
-    decided = undecided = 0
+    counts = check_unicode_values(vals, text, raws)
+    print(dict(counts))
+    assert counts["decided"] > 5000 and counts["undecided: SpecialCasing or unassigned"] > 100, counts
+
+
+UNICODE_PATHS = ["s.@case:upper", "s|@case:lower", "s.@strip"]
+
+
+def check_unicode_values(vals, text, raws):
+    """Values of UNICODE_PATHS on documents {"s":raw,"n":1}: each equals the Go
+    restatement's (tests/test_unicode_case.py) byte for byte, or is UNDECIDED exactly where
+    that restatement declines (SpecialCasing, code points unassigned in its tables)."""
+    from test_unicode_case import Undecided, go_case, go_strip
+
+    fns = [lambda r: go_case(r, True), lambda r: go_case(r, False), go_strip]
+    counts = collections.Counter()
     for k, raw in enumerate(raws):
+        doc = b'{"s":' + raw + b',"n":1}'
         for j, f in enumerate(fns):
             try:
                 want = f(raw)
             except Undecided:
-                assert (int(vals[k, j, 2]) & 0xFF) == 255, (paths[j], raw)
-                undecided += 1
+                assert (int(vals[k, j, 2]) & 0xFF) == 255, (UNICODE_PATHS[j], raw)
+                counts["undecided: SpecialCasing or unassigned"] += 1
                 continue
             st, ln, tt = (int(x) for x in vals[k, j])
-            assert (tt & 0xFF) == 3, (paths[j], raw, vals[k, j])
-            got = (text[k].tobytes() if (tt >> 8) & 4 else docs[k])[st:st + ln]
-            assert got == want[:len(got)] and len(got) >= min(len(want), 2), (paths[j], raw, got, want)
-            decided += 1
-    assert decided > 5000 and undecided > 100, (decided, undecided)
+            assert (tt & 0xFF) == 3, (UNICODE_PATHS[j], raw, vals[k, j])
+            got = (text[k].tobytes() if (tt >> 8) & 4 else doc)[st:st + ln]
+            assert got == want, (UNICODE_PATHS[j], raw, got, want)
+            counts["decided"] += 1
+    return counts

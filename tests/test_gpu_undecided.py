@@ -1,8 +1,9 @@
 """GPU: the UNDECIDED fraction on a realistic selector mix (tests/undecided_mix.py: the
 selectors of the reference's user guides on Authorization-JSON documents) through the
-kernels, one multi-tenant batch: 0 on ASCII documents; with non-ASCII user names (é, ß),
-only the requests whose ruleset applies @case to a SpecialCasing character (ß), every
-request both sides decide equal to the oracle (which restates @case for ASCII only). Rulesets with a
+kernels, one multi-tenant batch: 0 on ASCII documents and 0 with non-ASCII user names (é,
+ß: Go's simple case mapping keeps ß, ajx_unicode.h); every request the oracle decides
+equal to it, and the ones it leaves undecided (it restates @case for ASCII only) equal to
+tests/test_unicode_case.py's Go restatement. Rulesets with a
 by-design-unsupported form are skipped by the other random GPU tests; here they are
 counted: every such pattern is one of undecided_mix.BY_DESIGN_UNSUPPORTED's forms."""
 import random
@@ -23,7 +24,7 @@ def ctx():
     return runtime.Context(0)
 
 
-def _batch(ctx, non_ascii):
+def _batch(ctx, non_ascii, full=False):
     from authorino_amd import runtime
 
     rng = random.Random(31 + non_ascii)
@@ -44,7 +45,7 @@ def _batch(ctx, non_ascii):
     und = tri == runtime.UNDECIDED
     ok = ~und & (otri != runtime.UNDECIDED)
     assert np.array_equal(tri[ok], otri[ok]) and np.array_equal(err[ok], oerr[ok])
-    return docs, specs, sor, und
+    return (docs, specs, sor, und, tri, otri) if full else (docs, specs, sor, und)
 
 
 def test_no_undecided_on_ascii_documents(ctx):
@@ -52,14 +53,24 @@ def test_no_undecided_on_ascii_documents(ctx):
     assert und.sum() == 0
 
 
-def test_undecided_only_under_unicode_case_mapping(ctx):
-    docs, specs, sor, und = _batch(ctx, True)
-    frac = und.mean()
-    for i in np.nonzero(und)[0].tolist():
+def test_no_undecided_under_unicode_case_mapping(ctx):
+    import json
+
+    from authorino_amd import runtime
+    from test_unicode_case import go_case
+
+    docs, specs, sor, und, tri, otri = _batch(ctx, True, full=True)
+    assert und.sum() == 0, np.nonzero(und)[0][:10]
+    checked = 0
+    for i in np.nonzero(otri == runtime.UNDECIDED)[0].tolist():
         pats = specs[sor[i]][0]
-        assert any("@case" in s for s, _, _ in pats) and "ß".encode() in docs[i], (pats, docs[i][:200])
-    print("undecided fraction with non-ASCII user names:", frac)
-    assert 0 < frac < 0.1
+        assert pats == [("auth.identity.username.@case:upper", 1, "JOHN1")], (pats, docs[i][:200])
+        user = json.loads(docs[i])["auth"]["identity"]["username"]
+        assert go_case(user.encode(), True) != b"JOHN1"  # (a name with é / ß: never equal)
+        assert tri[i] == 0, (user, tri[i])
+        checked += 1
+    print({"requests": len(docs), "undecided": int(und.sum()), "non-ASCII @case checked against Go": checked})
+    assert checked > 0
 
 
 def test_by_design_unsupported_forms(ctx):

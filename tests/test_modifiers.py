@@ -63,7 +63,7 @@ def _chain(rng):
 @pytest.mark.parametrize("seed", [0, 1, 2, 3])
 def test_modifier_chains_match_oracle(seed):
     rng = random.Random(900 + seed)
-    checked = undecided = 0
+    checked = 0
     for _ in range(250):
         sel = _chain(rng)
         for _ in range(4):
@@ -80,12 +80,9 @@ def test_modifier_chains_match_oracle(seed):
             hr = H.HostRuleset(pats, nodes, 2)
             assert hr.status == [0, 0], (sel, hr.status)
             t, _, res = hr.eval(d)
-            if 3 in res:
-                undecided += 1
-                continue
-            assert res == [1, 0], (sel, d, w, res)
+            assert res == [1, 0], (sel, d, w, res)  # (decided: no reason for UNDECIDED here)
             checked += 1
-    assert checked > 300 and undecided <= checked // 5, (checked, undecided)
+    assert checked > 300, checked
 
 
 def _check_select(hr, p, d, want, text):
@@ -105,7 +102,7 @@ def test_select_value_text_matches_oracle(seed):
     the final Result's type and raw text, copied into the request's text slot, equal the
     oracle's gjson.Get with the same modifiers (json.go:96-151 ReplaceJSONPlaceholders)."""
     rng = random.Random(1900 + seed)
-    checked = undecided = 0
+    checked = 0
     for _ in range(200):
         sel = _chain(rng)
         hr = None
@@ -120,11 +117,9 @@ def test_select_value_text_matches_oracle(seed):
                 assert hr.status == [0], sel
             if want is None:
                 continue
-            if _check_select(hr, 0, d, want, bytearray(4096)):
-                checked += 1
-            else:
-                undecided += 1
-    assert checked > 300 and undecided <= checked // 5, (checked, undecided)
+            assert _check_select(hr, 0, d, want, bytearray(4096)), ("undecided", sel, d)
+            checked += 1
+    assert checked > 300, checked
 
 
 def test_select_value_lists_and_slot_overflow():

@@ -4,8 +4,11 @@ with the generated ajx_unicode.h, host build) against an independent restatement
 Go's `range` decoding (invalid / truncated / overlong / surrogate sequences are U+FFFD,
 width 1) via Python's strict UTF-8 decoder, the simple case mapping from str.upper() /
 str.lower() where it is one character, IsPrint as str.isprintable() (L M N P S and the
-ASCII space). Code points unassigned in this Python's Unicode (13.0; Go 1.21 has 15.0)
-and SpecialCasing characters must come back UNDECIDED, never guessed."""
+ASCII space). Go maps case with UnicodeData's simple mappings only: where Python's
+mapping is several characters (SpecialCasing.txt) the simple one is the one-character
+titlecase, or the character itself, and U+0130's lowercase is "i" (the KATs below pin
+these against Go's documented results). Code points unassigned in this Python's Unicode
+(13.0; Go 1.21 has 15.0) must come back UNDECIDED, never guessed (parity unpinned)."""
 import json
 import random
 import unicodedata
@@ -41,8 +44,19 @@ class Undecided(Exception):
 
 
 def _vouch(c):
-    if ord(c) >= 0x80 and (unicodedata.category(c) == "Cn" or len(c.upper()) != 1 or len(c.lower()) != 1):
+    if ord(c) >= 0x80 and unicodedata.category(c) == "Cn":
         raise Undecided()
+
+
+def _simple(c, upper):
+    """unicode.ToUpper / ToLower: the simple mapping (one character)."""
+    m = c.upper() if upper else c.lower()
+    if len(m) == 1:
+        return m
+    if not upper:
+        return "i"  # (U+0130, the one multi-character lowercase)
+    t = c.title()
+    return t if len(t) == 1 else c
 
 
 def go_case(raw: bytes, upper: bool) -> bytes:
@@ -51,7 +65,7 @@ def go_case(raw: bytes, upper: bool) -> bytes:
     out = []
     for c, _ in _runes(raw):
         _vouch(c)
-        out.append(c.upper() if upper else c.lower())
+        out.append(_simple(c, upper))
     return "".join(out).encode("utf-8", "surrogatepass")
 
 
@@ -106,16 +120,17 @@ def test_case_and_strip_on_unicode_match_go(seed):
             st, ln, tt = out
             src = bytes(text) if (tt >> 8) & 4 else d
             got = src[st:st + ln]
-            # (the Result of Parse(output): the string token, up to its closing quote)
-            assert got == want[:len(got)] and len(got) >= min(len(want), 2), (p, raw, got, want)
+            assert got == want, (p, raw, got, want)
             decided += 1
-    assert decided > 2000 and undecided > 50, (decided, undecided)
+    assert decided > 2000 and undecided > 20, (decided, undecided)
 
 
 def test_unicode_kats():
     """Go's behaviour on a few known cases (strings.ToUpper / ToLower / IsPrint)."""
     cases = [("s.@case:upper", "é ſ ı ǆ", "É S I Ǆ"), ("s.@case:lower", "ÉKKΣ", "ékkσ"),
-             ("s.@case:upper", "straße", None), ("s.@case:lower", "İ", None),  # (SpecialCasing)
+             ("s.@case:upper", "straße", "STRAßE"), ("s.@case:lower", "İSTANBUL", "istanbul"),  # (SpecialCasing)
+             ("s.@case:upper", "ﬁ ŉ ǰ ΐ ᾳ ᾈ ῷ", "ﬁ ŉ ǰ ΐ ᾼ ᾈ ῷ"), ("s.@case:lower", "ᾼ ᾈ", "ᾳ ᾀ"),
+             ("s.@case:upper", "\u0870", None),  # (Arabic, Unicode 14.0: unassigned in 13.0, undecided)
              ("s.@strip", "a\u00a0b\u00adc\u200bd", "abcd"), ("s.@strip", "x€漢😀", "x€漢😀")]
     for path, text, want in cases:
         d = json.dumps({"s": text}, ensure_ascii=False).encode()

@@ -43,7 +43,7 @@ BY_DESIGN_UNSUPPORTED = [
 def make_doc(rng: random.Random, non_ascii: bool = False) -> bytes:
     user = rng.choice(["john", "jane", "alice", "bob"]) + str(rng.randrange(100))
     if non_ascii and rng.random() < 0.5:
-        user += rng.choice(["é", "ß"])  # (ß: SpecialCasing, not vouched for by the device tables)
+        user += rng.choice(["é", "ß"])  # (ß: SpecialCasing; Go's simple mapping keeps it)
     review = {"kind": "AdmissionReview", "request": {
         "userInfo": {"username": "system:serviceaccount:" + user}, "object": {"metadata": {
             "namespace": rng.choice(["authorino", "default", "kube-system"])}}}}
