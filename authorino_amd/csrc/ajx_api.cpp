@@ -6,6 +6,7 @@
 #include <cstring>
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -20,6 +21,7 @@ struct authjx_ruleset {
     int device = 0;
     uint8_t* d_blob = nullptr;
     ajx::CompiledRuleset c;
+    bool stream_ok = false;  // the streaming kernel takes it (ajx::stream_eligible)
     // workspaces (by registry id) whose stream has run a batch over this ruleset:
     // authjx_free waits for their last batch instead of the whole device
     std::mutex mu;
@@ -30,15 +32,32 @@ struct authjx_ruleset {
     }
 };
 
+// The end-of-batch event of a workspace, shared with the registry (authjx_free waits on
+// it outside any lock): destroyed when the last holder lets go.
+struct EndEvent {
+    hipEvent_t ev = nullptr;
+    ~EndEvent() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
+
 // Per-stream scratch of a context: every distinct stream a context is called with gets
 // its own set table, slow list, capture rows and request order, so batches on two
 // streams of one context never share a buffer; calls on one stream take its mutex
 // (their kernels are ordered by the stream anyway).
+//
+// Lifetime: every user (a call through WsLock, the last_* readers) holds a reference,
+// taken and dropped under ctx->mu. Releasing the stream (authjx_release_stream, a
+// batcher's private streams) retires the workspace: it leaves ctx->ws and ctx->last_ws at
+// once, and whoever drops the last reference destroys it.
 struct Workspace {
     hipStream_t stream = nullptr;
     uint64_t id = 0;  // registry id (ruleset users)
+    uint32_t refs = 0;     // (ctx->mu)
+    bool retired = false;  // (ctx->mu)
     std::mutex mu;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // ev1: end of the last batch on this stream
+    std::shared_ptr<EndEvent> end;            // owns ev1
     // the ruleset pointer table the kernels index by set_of_req: two slots (device + pinned
     // source each), so a batch over another ruleset list fills the slot the batch before
     // the last one used (its event, not a stream synchronize, guards the reuse)
@@ -66,10 +85,10 @@ struct Workspace {
 };
 
 namespace {
-// live workspaces: id -> (device, end-of-last-batch event); authjx_free looks its
-// ruleset's users up here (an id that is gone belongs to a context already shut down)
+// live workspaces: id -> end-of-last-batch event; authjx_free looks its ruleset's users
+// up here (an id that is gone belongs to a workspace already destroyed)
 std::mutex g_reg_mu;
-std::vector<std::pair<uint64_t, std::pair<int, hipEvent_t>>> g_reg;
+std::vector<std::pair<uint64_t, std::shared_ptr<EndEvent>>> g_reg;
 uint64_t g_next_ws = 1;
 }  // namespace
 
@@ -87,18 +106,30 @@ struct authjx_ctx {
     int len_sort = 1;         // order requests by length class before the single-pass kernel
     int no_tenant_stage = 0;  // profiling: multi-tenant batches read tables from global memory
     int force_scan = 0;
+    // batches of up to this many requests go to the streaming kernel (latency: several
+    // waves per document span), larger ones to the lean / multi-tenant kernels
+    uint32_t stream_max_n = 4096;
     int ablate = 0;  // profiling / comparison only: 41 the lean single-pass kernel where the
-                     // streaming kernel would run, 50 / 51 the streaming kernel's
-                     // structural pass alone / without its fold, 1..3 / 10..12
-                     // token-scanner ablations and workgroup sizes
+                     // streaming kernel would run, 52 the streaming kernel for a one-ruleset
+                     // batch of any size, 50 / 51 its structural pass alone / without its
+                     // fold, 1..3 / 10..12 token-scanner ablations and workgroup sizes
 };
 
 namespace {
 
-#define HIP_OK(x)                                   \
-    do {                                            \
-        hipError_t e_ = (x);                        \
-        if (e_ != hipSuccess) return AUTHJX_EDEVICE; \
+// the last HIP error an entry point returned AUTHJX_EDEVICE for, on this thread
+// (authjx_debug_last_error)
+thread_local hipError_t t_last_hip = hipSuccess;
+thread_local int t_last_line = 0;
+
+#define HIP_OK(x)                  \
+    do {                           \
+        hipError_t e_ = (x);       \
+        if (e_ != hipSuccess) {    \
+            t_last_hip = e_;       \
+            t_last_line = __LINE__; \
+            return AUTHJX_EDEVICE; \
+        }                          \
     } while (0)
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -109,15 +140,17 @@ Workspace* workspace_of(authjx_ctx* ctx, hipStream_t s) {
         if (w->stream == s) return w;
     Workspace* w = new Workspace();
     w->stream = s;
-    if (hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->ev1) != hipSuccess) {
+    w->end = std::make_shared<EndEvent>();
+    if (hipEventCreate(&w->ev0) != hipSuccess || hipEventCreate(&w->end->ev) != hipSuccess) {
         if (w->ev0) (void)hipEventDestroy(w->ev0);
         delete w;
         return nullptr;
     }
+    w->ev1 = w->end->ev;
     {
         std::lock_guard<std::mutex> lock(g_reg_mu);
         w->id = g_next_ws++;
-        g_reg.push_back({w->id, {ctx->device, w->ev1}});
+        g_reg.push_back({w->id, w->end});
     }
     ctx->ws.push_back(w);
     return w;
@@ -141,8 +174,41 @@ void destroy_workspace(Workspace* w) {
     if (w->d_rows) (void)hipFree(w->d_rows);
     if (w->d_perm) (void)hipFree(w->d_perm);
     if (w->ev0) (void)hipEventDestroy(w->ev0);
-    if (w->ev1) (void)hipEventDestroy(w->ev1);
-    delete w;
+    delete w;  // (ev1 goes with the last holder of w->end)
+}
+
+// a reference to w (ctx->mu held by the caller)
+Workspace* ws_ref(Workspace* w) {
+    if (w) w->refs++;
+    return w;
+}
+// drops a reference; the last one of a retired workspace destroys it
+void ws_unref(authjx_ctx* ctx, Workspace* w) {
+    bool dead;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        dead = --w->refs == 0 && w->retired;
+    }
+    if (dead) destroy_workspace(w);  // (waits for the stream's last batch)
+}
+
+// retires the workspace of stream s (the caller holds no lock)
+void retire_stream(authjx_ctx* ctx, hipStream_t s) {
+    Workspace* w = nullptr;
+    bool dead = false;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        for (size_t i = 0; i < ctx->ws.size(); i++)
+            if (ctx->ws[i]->stream == s) {
+                w = ctx->ws[i];
+                ctx->ws.erase(ctx->ws.begin() + (long)i);
+                if (ctx->last_ws == w) ctx->last_ws = nullptr;
+                w->retired = true;
+                dead = w->refs == 0;
+                break;
+            }
+    }
+    if (dead) destroy_workspace(w);  // (else the call still on that stream does, when it ends)
 }
 
 int ensure_sets(Workspace* w, int device, const authjx_ruleset* const* sets, uint32_t n_sets) {
@@ -215,23 +281,48 @@ int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
 
 // a device call's workspace, locked: ctx->mu only while the workspace is looked up, not
 // while waiting for a busy stream's workspace (calls on the context's other streams, the
-// batcher's workers among them, go on meanwhile). A workspace lives until shutdown, or
-// until authjx_batcher_destroy for a batcher's private streams, which only its joined
-// workers used. Lock order: w->mu before ctx->mu.
+// batcher's workers among them, go on meanwhile). The reference taken with the lookup keeps
+// the workspace alive while this call waits for its mutex, even if its stream is released
+// meanwhile. Lock order: w->mu before ctx->mu.
 struct WsLock {
+    authjx_ctx* ctx;
     Workspace* w = nullptr;
     std::unique_lock<std::mutex> lock;
-    WsLock(authjx_ctx* ctx, void* stream) {
+    WsLock(authjx_ctx* c, void* stream) : ctx(c) {
         {
             std::lock_guard<std::mutex> g(ctx->mu);
-            w = workspace_of(ctx, stream ? (hipStream_t)stream : ctx->stream);
+            w = ws_ref(workspace_of(ctx, stream ? (hipStream_t)stream : ctx->stream));
         }
         if (w) {
             lock = std::unique_lock<std::mutex>(w->mu);
             std::lock_guard<std::mutex> g(ctx->mu);
-            ctx->last_ws = w;
+            if (!w->retired) ctx->last_ws = w;
         }
     }
+    ~WsLock() {
+        if (!w) return;
+        lock.unlock();
+        ws_unref(ctx, w);
+    }
+    WsLock(const WsLock&) = delete;
+    WsLock& operator=(const WsLock&) = delete;
+};
+
+// ctx->last_ws with a reference (the last_* readers)
+struct LastWs {
+    authjx_ctx* ctx;
+    Workspace* w = nullptr;
+    int force_scan = 0;
+    explicit LastWs(authjx_ctx* c) : ctx(c) {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        w = ws_ref(ctx->last_ws);
+        force_scan = ctx->force_scan;
+    }
+    ~LastWs() {
+        if (w) ws_unref(ctx, w);
+    }
+    LastWs(const LastWs&) = delete;
+    LastWs& operator=(const LastWs&) = delete;
 };
 
 // after the launches of a batch: ev1 marks its end on the stream; the rulesets record
@@ -290,7 +381,7 @@ void authjx_shutdown(authjx_ctx* ctx) {
     for (authjx_batcher* b : live) authjx_batcher_destroy(b);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (Workspace* w : ctx->ws) destroy_workspace(w);
+    for (Workspace* w : ctx->ws) destroy_workspace(w);  // (no call may run during shutdown)
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -298,25 +389,11 @@ void authjx_shutdown(authjx_ctx* ctx) {
 
 int authjx_release_stream(authjx_ctx* ctx, void* stream) {
     if (!ctx || !stream || (hipStream_t)stream == ctx->stream) return AUTHJX_EINVAL;
-    Workspace* w = nullptr;
-    {
-        std::lock_guard<std::mutex> g(ctx->mu);
-        for (size_t i = 0; i < ctx->ws.size(); i++)
-            if (ctx->ws[i]->stream == (hipStream_t)stream) {
-                w = ctx->ws[i];
-                ctx->ws.erase(ctx->ws.begin() + (long)i);
-                if (ctx->last_ws == w) ctx->last_ws = nullptr;
-                break;
-            }
-    }
-    if (!w) return AUTHJX_OK;
     (void)hipSetDevice(ctx->device);
-    {
-        std::lock_guard<std::mutex> g(w->mu);  // (a call still inside on that stream finishes first)
-    }
-    destroy_workspace(w);  // (waits for the stream's last batch)
+    retire_stream(ctx, (hipStream_t)stream);
     return AUTHJX_OK;
 }
+
 
 namespace {
 int finish_compile(authjx_ctx* ctx, authjx_ruleset* rs, int rc, const std::string& err, authjx_ruleset** out,
@@ -356,6 +433,7 @@ int finish_compile(authjx_ctx* ctx, authjx_ruleset* rs, int rc, const std::strin
     if (pattern_status)
         for (uint32_t i = 0; i < rs->c.n_patterns; i++) pattern_status[i] = rs->c.pattern_status[i];
     rs->device = ctx->device;
+    rs->stream_ok = ajx::stream_eligible(rs->c.blob.data(), (uint32_t)rs->c.blob.size());
     if (hipSetDevice(ctx->device) != hipSuccess ||
         hipMalloc(&rs->d_blob, rs->c.blob.size()) != hipSuccess ||
         hipMemcpy(rs->d_blob, rs->c.blob.data(), rs->c.blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -373,14 +451,17 @@ void authjx_free(authjx_ruleset* rs) {
     if (rs->d_blob) {
         (void)hipSetDevice(rs->device);
         // wait for the last batch of every stream that used this ruleset (not the device:
-        // other streams' batches and other work go on)
+        // other streams' batches and other work go on); the events are collected under the
+        // registry lock and waited on outside it
+        std::vector<std::shared_ptr<EndEvent>> evs;
         {
             std::lock_guard<std::mutex> lock(rs->mu);
             std::lock_guard<std::mutex> reg(g_reg_mu);
             for (uint64_t id : rs->users)
                 for (const auto& e : g_reg)
-                    if (e.first == id) (void)hipEventSynchronize(e.second.second);
+                    if (e.first == id) evs.push_back(e.second);
         }
+        for (const auto& e : evs) (void)hipEventSynchronize(e->ev);
         (void)hipFree(rs->d_blob);
     }
     delete rs;
@@ -414,12 +495,14 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     const uint32_t row_stride = 1 + max_sel;
     if (d_out_bitmap && bitmap_stride_words < need_words) return AUTHJX_EINVAL;
     int force_scan, ablate, len_sort, no_tenant_stage;
+    uint32_t stream_max_n;
     {
         std::lock_guard<std::mutex> g(ctx->mu);
         force_scan = ctx->force_scan;
         ablate = ctx->ablate;
         len_sort = ctx->len_sort;
         no_tenant_stage = ctx->no_tenant_stage;
+        stream_max_n = ctx->stream_max_n;
     }
     WsLock wl(ctx, stream);
     Workspace* w = wl.w;
@@ -428,10 +511,20 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     HIP_OK(hipSetDevice(ctx->device));
     int rc = ensure_sets(w, ctx->device, sets, n_sets);
     if (rc != AUTHJX_OK) return rc;
-    // the streaming kernel takes a one-ruleset batch whose ruleset has stream tables (its
-    // rows carry 4 more words: the eager decisions stage B reads)
-    const bool use_stream = !force_scan && n_sets == 1 && (ablate == 0 || ablate == 50 || ablate == 51) &&
-                            ajx::stream_eligible(sets[0]->c.blob.data(), (uint32_t)sets[0]->c.blob.size());
+    // the streaming kernel: small batches (latency; one request per wave for a multi-tenant
+    // batch) whose rulesets all have stream tables; any one-ruleset batch under kernel
+    // mode 50..52 (its rows carry 4 more words: the eager decisions stage B reads)
+    bool all_stream = true;
+    for (uint32_t i = 0; i < n_sets; i++) all_stream = all_stream && sets[i]->stream_ok;
+    const bool small = n <= stream_max_n;
+    const bool use_stream = !force_scan && all_stream &&
+                            ((ablate == 0 && small) || (n_sets == 1 && ablate >= 50 && ablate <= 52));
+    // requests per wave: 32 for throughput, fewer for a small batch (more waves share it)
+    uint32_t per = ajx::kStreamSpan;
+    if (n_sets > 1)
+        per = 1;
+    else if (ablate == 0)
+        per = std::max<uint32_t>(1u, std::min<uint32_t>(ajx::kStreamSpan, (n + 2047u) / 2048u));
     const uint32_t rows_stride = use_stream ? row_stride + 4u : row_stride;
     if (!force_scan) {
         rc = ensure_work(w, n, rows_stride);
@@ -447,7 +540,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
                (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagBufs) != 0;
     // capture rows kept for authjx_select_from_eval_device: one forest ruleset
     // (authjx_compile_forest), a full kernel
-    const bool full = ablate == 0 || ablate == 41 || (ablate >= 10 && ablate <= 12);
+    const bool full = ablate == 0 || ablate == 41 || ablate == 52 || (ablate >= 10 && ablate <= 12);
     const auto* h0 = reinterpret_cast<const ajx::RulesetHdr*>(sets[0]->c.blob.data());
     const bool keep_rows = !force_scan && n_sets == 1 && full && h0->pad1[0] != 0;
     w->rows_rs = keep_rows ? sets[0] : nullptr;
@@ -464,10 +557,10 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         // the streaming kernel (ajx_stream.h; ablate 50: its structural pass alone, 51: no
         // fold), its stage B over the d_perm buffer as the stage-B list
         w->rows_stride = rows_stride;
-        HIP_OK(ajx::launch_eval_stream(w->d_sets, (uint32_t)sets[0]->c.blob.size(), sets[0]->c.n_selectors, d_arena,
+        HIP_OK(ajx::launch_eval_stream(w->d_sets, d_set_of_req, (uint32_t)sets[0]->c.blob.size(), max_sel, d_arena,
                                        d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap,
                                        bitmap_stride_words, w->d_rows, rows_stride, keep_rows, w->d_perm, w->d_slow,
-                                       w->d_slow + 1, s, ablate == 50 ? 1 : ablate == 51 ? 2 : 0, mods));
+                                       w->d_slow + 1, s, ablate == 50 ? 1 : ablate == 51 ? 2 : 0, mods, per));
     } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
         // caller's bucketing by AuthConfig), a full kernel, batches worth sorting
@@ -633,6 +726,24 @@ int authjx_debug_ablate(authjx_ctx* ctx, int mode) {
 }
 
 
+// Profiling only (not in authjx.h): batches of up to n requests take the streaming kernel
+// (default 4096; 0: never)
+int authjx_debug_stream_max(authjx_ctx* ctx, uint32_t n) {
+    if (!ctx) return AUTHJX_EINVAL;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->stream_max_n = n;
+    return AUTHJX_OK;
+}
+
+// Diagnostics (not in authjx.h): the HIP error behind this thread's last AUTHJX_EDEVICE and
+// the ajx_api.cpp line that saw it ("" when none)
+const char* authjx_debug_last_error(void) {
+    static thread_local char buf[160];
+    if (t_last_hip == hipSuccess) return "";
+    std::snprintf(buf, sizeof buf, "%s (ajx_api.cpp:%d)", hipGetErrorString(t_last_hip), t_last_line);
+    return buf;
+}
+
 // Profiling only (not in authjx.h): the length-bucketed request order off (0), for
 // single-ruleset batches (1, default) or for every batch (2).
 int authjx_debug_len_sort(authjx_ctx* ctx, int on) {
@@ -663,14 +774,9 @@ int authjx_set_exact_scan(authjx_ctx* ctx, int force) {
 
 int64_t authjx_last_exact_count(authjx_ctx* ctx) {
     if (!ctx) return AUTHJX_EINVAL;
-    Workspace* w;
-    int force_scan;
-    {
-        std::lock_guard<std::mutex> g(ctx->mu);
-        w = ctx->last_ws;
-        force_scan = ctx->force_scan;
-    }
-    if (force_scan || !w) return -1;
+    LastWs ref(ctx);
+    Workspace* w = ref.w;
+    if (ref.force_scan || !w) return -1;
     std::lock_guard<std::mutex> lock(w->mu);
     if (!w->d_slow || !w->ran) return -1;
     uint32_t c = 0;
@@ -682,11 +788,8 @@ int64_t authjx_last_exact_count(authjx_ctx* ctx) {
 
 float authjx_last_kernel_ms(authjx_ctx* ctx) {
     if (!ctx) return 0.f;
-    Workspace* w;
-    {
-        std::lock_guard<std::mutex> g(ctx->mu);
-        w = ctx->last_ws;
-    }
+    LastWs ref(ctx);
+    Workspace* w = ref.w;
     if (!w) return 0.f;
     std::lock_guard<std::mutex> lock(w->mu);
     float ms = 0.f;
@@ -874,17 +977,7 @@ void authjx_batcher_destroy(authjx_batcher* b) {
         if (L.stream) (void)hipStreamSynchronize(L.stream);
         if (L.h_buf) (void)hipHostFree(L.h_buf);
         if (L.d_buf) (void)hipFree(L.d_buf);
-        {
-            // the context keeps the stream's workspace until shutdown; the stream goes now
-            std::lock_guard<std::mutex> g(b->ctx->mu);
-            for (size_t i = 0; i < b->ctx->ws.size(); i++)
-                if (b->ctx->ws[i]->stream == L.stream) {
-                    if (b->ctx->last_ws == b->ctx->ws[i]) b->ctx->last_ws = nullptr;
-                    destroy_workspace(b->ctx->ws[i]);
-                    b->ctx->ws.erase(b->ctx->ws.begin() + (long)i);
-                    break;
-                }
-        }
+        if (L.stream) retire_stream(b->ctx, L.stream);  // (only the joined workers used it)
         if (L.stream) (void)hipStreamDestroy(L.stream);
     }
     delete b;

@@ -513,9 +513,12 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
 // rulesets, for authjx_select_from_eval_device): every request's row is written (slow
 // ones: kRowSlow), those with an open record through stage B. Rows: the wave-interleaved
 // layout at work-item r. Profiling: MODE 1 the structural pass only, 2 no fold.
-// Dynamic LDS: [blob copy] [per wave: WaveLds, capture rows, eager decisions]
-template <int MODE>
+// Dynamic LDS: [blob copy] [per wave: WaveLds, capture rows, eager decisions].
+// MT (multi-tenant latency batches): one request per wave (per = 1) under its own
+// ruleset sets[set_of_req[r]], its tables read from global memory (L2), no blob copy.
+template <int MODE, bool MT = false>
 __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __restrict__ sets,
+                                                       const uint32_t* __restrict__ set_of_req,
                                                        const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ offs,
                                                        const uint32_t* __restrict__ lens, uint32_t n,
@@ -524,20 +527,26 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
                                                        uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
                                                        uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t wave_off,
                                                        uint32_t wave_bytes, uint64_t* __restrict__ rows_out,
-                                                       uint32_t row_stride, uint32_t keep_rows) {
-    const uint8_t* blob = stage_blob<true>(sets[0]);
+                                                       uint32_t row_stride, uint32_t keep_rows, uint32_t per) {
     extern __shared__ uint4 s_stream_dyn[];
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const uint32_t span = blockIdx.x * (blockDim.x >> 6) + w;
+    const uint8_t* blob;
+    if constexpr (MT) {
+        if (span >= n) return;  // (wave-uniform; per = 1)
+        blob = sets[set_of_req[span]];
+    } else {
+        blob = stage_blob<true>(sets[0]);
+    }
     uint8_t* base = reinterpret_cast<uint8_t*>(s_stream_dyn) + wave_off + w * wave_bytes;
     stream::WaveLds& L = *reinterpret_cast<stream::WaveLds*>(base);
     uint64_t* rows = reinterpret_cast<uint64_t*>(base + sizeof(stream::WaveLds));
-    const uint32_t span = blockIdx.x * (blockDim.x >> 6) + w;
-    if (span * stream::kSpan >= n) return;  // (wave-uniform)
+    if (span * per >= n) return;  // (wave-uniform)
     const uint64_t *rowp = nullptr, *dwp = nullptr;
-    const uint32_t res = stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm,
-                                                 stride, &rowp, &dwp);
-    const uint32_t r = span * stream::kSpan + l;
-    if (l >= stream::kSpan || r >= n || MODE != 0) return;
+    const uint32_t res = stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
+                                                 out_bm, stride, &rowp, &dwp);
+    const uint32_t r = span * per + l;
+    if (l >= per || r >= n || MODE != 0) return;
     const RowRef o = wave_row(rows_out, row_stride, r);
     if (res == stream::R_SLOW) {
         slow_ids[atomicAdd(slow_count, 1u)] = r;
@@ -558,8 +567,11 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
 }
 
 // Stage B of the streaming kernel: one work-item per request on the stage-B list, on its
-// row in HBM (stream::finish_full); what it can not decide goes to the slow list.
+// row in HBM (stream::finish_full); what it can not decide goes to the slow list. MT: each
+// request's own ruleset, read from global memory.
+template <bool MT = false>
 __global__ __launch_bounds__(256) void ajx_stream_finish(const uint8_t* const* __restrict__ sets,
+                                                         const uint32_t* __restrict__ set_of_req,
                                                          const uint8_t* __restrict__ arena,
                                                          const uint64_t* __restrict__ offs,
                                                          const uint32_t* __restrict__ lens,
@@ -569,10 +581,11 @@ __global__ __launch_bounds__(256) void ajx_stream_finish(const uint8_t* const* _
                                                          uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
                                                          int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
                                                          uint32_t stride) {
-    const uint8_t* blob = stage_blob<true>(sets[0]);
+    const uint8_t* blob0 = MT ? nullptr : stage_blob<true>(sets[0]);
     const uint32_t cnt = *stage_list;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
         const uint32_t r = stage_list[1u + i];
+        const uint8_t* blob = MT ? sets[set_of_req[r]] : blob0;
         if (!stream::finish_full(r, blob, arena + offs[r], lens[r], wave_row(rows, row_stride, r), out_tri, out_err,
                                  out_bm, stride))
             slow_ids[atomicAdd(slow_count, 1u)] = r;
@@ -585,32 +598,31 @@ bool stream_eligible(const uint8_t* host_blob, uint32_t blob_bytes) {
            h->n_selectors <= kFastMaxSelectors;
 }
 
-// workgroup of 4 or 8 waves: the size that fits the most waves per CU next to the blob copy
-static uint32_t stream_block(uint32_t blob_bytes, uint32_t wave_bytes) {
-    const uint32_t stage = (blob_bytes + 15u) & ~15u;
-    uint32_t best = 256, best_w = 0;
-    for (uint32_t b = 256; b <= 512; b *= 2) {
-        const uint32_t lds = stage + (b / 64) * wave_bytes;
-        uint32_t wv = lds <= 160u * 1024u ? (160u * 1024u / lds) * (b / 64) : 0u;
-        if (wv > 32) wv = 32;
-        if (wv > best_w) best = b, best_w = wv;
-    }
-    return best;
-}
+static_assert(kStreamSpan == stream::kSpan, "requests per wave");
 
-hipError_t launch_eval_stream(const uint8_t* const* d_sets, uint32_t blob_bytes, uint32_t n_selectors,
-                              const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+// 4-wave workgroups (the kernel's launch bounds), each with its own blob copy
+constexpr uint32_t kStreamBlock = 256;
+
+hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t blob_bytes,
+                              uint32_t n_selectors, const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                               uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                               uint32_t row_stride, bool keep_rows, uint32_t* d_stage_list, uint32_t* d_slow_count,
-                              uint32_t* d_slow_ids, hipStream_t stream, int mode, bool mods) {
+                              uint32_t* d_slow_ids, hipStream_t stream, int mode, bool mods, uint32_t per) {
     if (n == 0) return hipSuccess;
     if (row_stride < 5u + n_selectors) return hipErrorInvalidValue;
+    const bool mt = d_set_of_req != nullptr;
+    if (mt) {
+        if (mode != 0) return hipErrorInvalidValue;
+        per = 1;
+        blob_bytes = 0;  // (no blob copy: each wave reads its ruleset from global memory)
+    }
     const uint32_t wave_off = (blob_bytes + 15u) & ~15u;
     const uint32_t wave_bytes = (stream::lds_bytes(n_selectors) + 15u) & ~15u;
-    const uint32_t block = stream_block(blob_bytes, wave_bytes);
+    const uint32_t block = kStreamBlock;
     const uint32_t lds = wave_off + (block / 64) * wave_bytes;
     if (lds > 160u * 1024u) return hipErrorInvalidValue;
-    const uint32_t spans = (n + stream::kSpan - 1) / stream::kSpan;
+    if (per == 0 || per > stream::kSpan) per = stream::kSpan;
+    const uint32_t spans = (n + per - 1) / per;
     const uint32_t grid = (spans + block / 64 - 1) / (block / 64);
     hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
@@ -620,33 +632,44 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, uint32_t blob_bytes,
         for (const void* k : {reinterpret_cast<const void*>(&ajx_scan_stream<0>),
                               reinterpret_cast<const void*>(&ajx_scan_stream<1>),
                               reinterpret_cast<const void*>(&ajx_scan_stream<2>),
-                              reinterpret_cast<const void*>(&ajx_stream_finish)}) {
+                              reinterpret_cast<const void*>(&ajx_scan_stream<0, true>),
+                              reinterpret_cast<const void*>(&ajx_stream_finish<false>),
+                              reinterpret_cast<const void*>(&ajx_stream_finish<true>)}) {
             const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (r != hipSuccess) return r;
         }
         return hipSuccess;
     });
     if (e != hipSuccess) return e;
-#define AJX_STREAM_LAUNCH(M)                                                                                       \
-    hipLaunchKernelGGL((ajx_scan_stream<M>), dim3(grid), dim3(block), lds, stream, d_sets, d_arena, d_offs, d_lens, n, \
+#define AJX_STREAM_LAUNCH(M, T)                                                                               \
+    hipLaunchKernelGGL((ajx_scan_stream<M, T>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena, \
+                       d_offs, d_lens, n, \
                        d_slow_count, d_slow_ids, d_stage_list, d_tri, d_err, d_bm, stride, wave_off, wave_bytes,      \
-                       d_rows, row_stride, keep_rows ? 1u : 0u)
-    if (mode == 1)
-        AJX_STREAM_LAUNCH(1);
+                       d_rows, row_stride, keep_rows ? 1u : 0u, per)
+    if (mt)
+        AJX_STREAM_LAUNCH(0, true);
+    else if (mode == 1)
+        AJX_STREAM_LAUNCH(1, false);
     else if (mode == 2)
-        AJX_STREAM_LAUNCH(2);
+        AJX_STREAM_LAUNCH(2, false);
     else
-        AJX_STREAM_LAUNCH(0);
+        AJX_STREAM_LAUNCH(0, false);
 #undef AJX_STREAM_LAUNCH
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mode != 0) return hipSuccess;
     // stage B and the exact scan over their lists (grid-stride: the lists' lengths are on the device)
-    const uint32_t fgrid = spans < 2048 ? (spans * stream::kSpan + 255) / 256 : 4096;
-    hipLaunchKernelGGL(ajx_stream_finish, dim3(fgrid), dim3(256), wave_off, stream, d_sets, d_arena, d_offs, d_lens,
-                       d_stage_list, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
+    const uint32_t fgrid = n < 2048u * 256u ? (n + 255) / 256 : 4096;
+    if (mt)
+        hipLaunchKernelGGL(ajx_stream_finish<true>, dim3(fgrid), dim3(256), 0, stream, d_sets, d_set_of_req, d_arena,
+                           d_offs, d_lens, d_stage_list, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
+                           d_bm, stride);
+    else
+        hipLaunchKernelGGL(ajx_stream_finish<false>, dim3(fgrid), dim3(256), wave_off, stream, d_sets, nullptr,
+                           d_arena, d_offs, d_lens, d_stage_list, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri,
+                           d_err, d_bm, stride);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t sgrid = spans < 1024 ? 2 * ((spans * 64 + 255) / 256) : 4096;
-    launch_slow_list(mods, sgrid, stream, d_sets, nullptr, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids, d_tri,
+    const uint32_t sgrid = n < 1024u * 128u ? 2 * ((n + 255) / 256) : 4096;
+    launch_slow_list(mods, sgrid, stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids, d_tri,
                      d_err, d_bm, stride);
     return hipGetLastError();
 }

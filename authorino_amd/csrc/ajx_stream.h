@@ -1023,19 +1023,19 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
 
 enum : uint32_t { R_DONE = 0, R_SLOW = 1, R_STAGE_B = 2 };
 
-// The whole span for this lane: setup, the steps, then request r = span * kSpan + l
-// (l < kSpan): R_DONE (decided and folded; its row holds captures with possibly open
-// ends), R_SLOW (the exact scan decides it) or R_STAGE_B (its row and eager words, *row_out
-// / *dw_out, go to finish_full).
+// The whole span for this lane: setup, the steps, then request r = span * per + l
+// (l < per <= kSpan requests per span): R_DONE (decided and folded; its row holds captures
+// with possibly open ends), R_SLOW (the exact scan decides it) or R_STAGE_B (its row and
+// eager words, *row_out / *dw_out, go to finish_full).
 template <int MODE = 0>
 AJX_HD uint32_t scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const uint8_t* __restrict__ arena,
                           const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
-                          uint32_t span, uint32_t l, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-                          uint64_t* __restrict__ out_bm, uint32_t stride, const uint64_t** row_out,
-                          const uint64_t** dw_out) {
+                          uint32_t span, uint32_t per, uint32_t l, uint8_t* __restrict__ out_tri,
+                          int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm, uint32_t stride,
+                          const uint64_t** row_out, const uint64_t** dw_out) {
     const Tabs T = tabs_of(blob);
-    const uint32_t r = span * kSpan + l;
-    const bool my = l < kSpan && r < n;
+    const uint32_t r = span * per + l;
+    const bool my = l < per && r < n;
     const uint64_t off = my ? offs[r] : 0ull;
     const uint32_t len = my ? lens[r] : 0u;
     uint32_t my_start, total;

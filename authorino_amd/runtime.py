@@ -172,6 +172,8 @@ def load_library(path: str = LIB_PATH):
         L.authjx_pack_json.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64,
                                        C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32]
         L.authjx_pack_json.restype = C.c_int
+        L.authjx_debug_last_error.argtypes = []
+        L.authjx_debug_last_error.restype = C.c_char_p
         _lib = L
         return L
 
@@ -179,7 +181,10 @@ def load_library(path: str = LIB_PATH):
 def _check(rc: int, what: str):
     if rc != 0:
         names = {-1: "EINVAL", -2: "ENOMEM", -3: "EDEVICE", -4: "ELIMIT", -5: "ETIMEDOUT", -6: "ECLOSED"}
-        raise AuthjxError(f"{what} failed: {names.get(rc, rc)}")
+        detail = ""
+        if rc == -3 and _lib is not None:  # (the HIP error behind it, on this thread)
+            detail = " (%s)" % _lib.authjx_debug_last_error().decode()
+        raise AuthjxError(f"{what} failed: {names.get(rc, rc)}{detail}")
 
 
 def _b(s) -> bytes:
@@ -241,11 +246,20 @@ class Context:
         _check(load_library().authjx_set_exact_scan(self._h, 1 if force else 0), "authjx_set_exact_scan")
 
     def set_kernel_mode(self, mode: int) -> None:
-        """Select the kernel: 0 the single-pass kernel (default), 20 the lane kernel; other
-        values are profiling ablations whose outputs are meaningless. Not part of authjx.h."""
+        """Select the kernel: 0 the default (the streaming kernel for small batches, the lean
+        or multi-tenant kernel otherwise), 41 the lean kernel for every batch, 52 the
+        streaming kernel for every one-ruleset batch; 50 / 51 and others are profiling
+        ablations whose outputs are meaningless. Not part of authjx.h."""
         L = load_library()
         L.authjx_debug_ablate.argtypes = [C.c_void_p, C.c_int]
         _check(L.authjx_debug_ablate(self._h, int(mode)), "authjx_debug_ablate")
+
+    def set_stream_max(self, n: int) -> None:
+        """Batches of up to n requests take the streaming kernel (default 4096; 0 never).
+        Profiling; not part of authjx.h."""
+        L = load_library()
+        L.authjx_debug_stream_max.argtypes = [C.c_void_p, C.c_uint32]
+        _check(L.authjx_debug_stream_max(self._h, int(n)), "authjx_debug_stream_max")
 
     def last_exact_count(self) -> int:
         """Requests of the last batch the single-pass kernel handed to the exact scan."""

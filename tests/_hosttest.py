@@ -28,8 +28,11 @@ class _Tree(C.Structure):
 def lib():
     global _L
     if _L is None:
-        subprocess.run(["make", "-s", "-C", _NATIVE], check=True)
-        L = C.CDLL(os.path.join(_NATIVE, "libajx_hosttest.so"))
+        path = os.environ.get("AJX_HOSTTEST_LIB")  # (debugging: e.g. an ASan build of the same sources)
+        if not path:
+            subprocess.run(["make", "-s", "-C", _NATIVE], check=True)
+            path = os.path.join(_NATIVE, "libajx_hosttest.so")
+        L = C.CDLL(path)
         L.ht_compile.argtypes = [C.POINTER(_Tree), C.POINTER(C.c_int32), C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
         L.ht_compile.restype = C.c_void_p
         L.ht_free.argtypes = [C.c_void_p]
@@ -235,14 +238,15 @@ def json_valid(text) -> int:
     return lib().ht_json_valid(d, len(d))
 
 
-def eval_stream(hr, arena, offs, lens, mode=0, stride=2, dbg=None):
+def eval_stream(hr, arena, offs, lens, mode=0, stride=2, dbg=None, per=0):
     """The streaming scan (ajx_stream.h) over a batch on the host emulation of the wave,
     then its stage B: (tri, err, bitmap, slow) — slow[r] = 1 where request r goes to the
-    exact scan, 2 where stage B decided it; None when the ruleset has no stream tables."""
+    exact scan, 2 where stage B decided it; None when the ruleset has no stream tables.
+    per: requests per wave (0: 32)."""
     L = lib()
     if not getattr(L, "_stream_decl", False):
         L.ht_eval_stream.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
-                                     C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]
+                                     C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p, C.c_uint32]
         L.ht_eval_stream.restype = C.c_int
         L._stream_decl = True
     import numpy as np
@@ -257,7 +261,7 @@ def eval_stream(hr, arena, offs, lens, mode=0, stride=2, dbg=None):
     slow = np.zeros(n, np.uint8)
     rc = L.ht_eval_stream(hr._h, a.ctypes.data, offs.ctypes.data, lens.ctypes.data, n, tri.ctypes.data,
                           err.ctypes.data, bm.ctypes.data, stride, slow.ctypes.data, mode,
-                          None if dbg is None else dbg.ctypes.data)
+                          None if dbg is None else dbg.ctypes.data, per)
     if rc < 0:
         return None
     return tri, err, bm, slow

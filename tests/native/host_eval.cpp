@@ -326,7 +326,7 @@ extern "C" void ht_lean_counts(uint64_t* iters, uint64_t* subs) {
 // (out_tri[r] = proved). Returns -1 when the ruleset has no stream tables.
 extern "C" int ht_eval_stream(void* h, const uint8_t* arena, const uint64_t* offs, const uint32_t* lens, uint32_t n,
                               uint8_t* out_tri, int32_t* out_err, uint64_t* out_bm, uint32_t stride, uint8_t* out_slow,
-                              int mode, uint32_t* out_dbg) {
+                              int mode, uint32_t* out_dbg, uint32_t per) {
     const std::vector<uint8_t>& blob_v = ((HtRuleset*)h)->c.blob;
     const RulesetHdr* hd = (const RulesetHdr*)blob_v.data();
     if (!hd->off_stream) return -1;
@@ -335,7 +335,8 @@ extern "C" int ht_eval_stream(void* h, const uint8_t* arena, const uint64_t* off
     std::memcpy(blob_buf.data(), blob_v.data(), blob_v.size());
     const uint8_t* blob = (const uint8_t*)blob_buf.data();
     const uint32_t ns = hd->n_selectors;
-    const uint32_t spans = (n + stream::kSpan - 1) / stream::kSpan;
+    if (per == 0 || per > stream::kSpan) per = stream::kSpan;
+    const uint32_t spans = (n + per - 1) / per;
     std::vector<uint64_t> wl(stream::lds_bytes(ns) / 8 + 2);
     std::vector<uint64_t> stage_rows((size_t)n * (5 + ns));
     std::vector<uint32_t> stage_list;
@@ -348,13 +349,13 @@ extern "C" int ht_eval_stream(void* h, const uint8_t* arena, const uint64_t* off
             const uint64_t *rowp = nullptr, *dwp = nullptr;
             uint32_t res;
             if (mode == 1)
-                res = stream::scan_span<1>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm,
-                                           stride, &rowp, &dwp);
+                res = stream::scan_span<1>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
+                                           out_bm, stride, &rowp, &dwp);
             else
-                res = stream::scan_span<0>(L, rows, blob, arena, offs, lens, n, span, l, out_tri, out_err, out_bm,
-                                           stride, &rowp, &dwp);
-            const uint32_t r = span * stream::kSpan + l;
-            if (l >= stream::kSpan || r >= n) return;
+                res = stream::scan_span<0>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
+                                           out_bm, stride, &rowp, &dwp);
+            const uint32_t r = span * per + l;
+            if (l >= per || r >= n) return;
             out_slow[r] = res == stream::R_SLOW ? 1 : 0;
             if (res == stream::R_STAGE_B) {
                 uint64_t* o = stage_rows.data() + (size_t)r * (5 + ns);

@@ -50,3 +50,19 @@ def test_batcher_and_index_under_tsan(chain_bins):
     r = subprocess.run([chain_bins[1], "16", "300"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, (r.stdout[-2000:], r.stderr[-4000:])
     assert r.stdout.startswith("ok ") and "wrong 0" in r.stdout
+
+
+def test_workspace_lifetime_under_tsan():
+    """The C-ABI's per-stream workspaces (ajx_api.cpp) on a host stand-in of the HIP runtime
+    (tests/native/hipstub): evaluations on short-lived streams released while other threads
+    read authjx_last_exact_count / authjx_last_kernel_ms, a stream released while a call is
+    still on it, host-buffer batches with rulesets compiled and freed, a micro-batcher
+    created and destroyed — under ThreadSanitizer, no report. (The same driver on the
+    round-3 code, which freed a released workspace under a waiting reader, reported
+    use-after-free races.)"""
+    subprocess.run(["make", "-s", "-C", _NATIVE, "tsan_api"], check=True, timeout=600)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([os.path.join(_NATIVE, "tsan_api"), "150"], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, (r.stdout[-2000:], r.stderr[-4000:])
+    assert r.stdout.startswith("ok ") and "errors 0" in r.stdout

@@ -26,13 +26,13 @@ def _pack(docs):
     return arena, offs, lens
 
 
-def _check(pats, nodes, root, arena, offs, lens, allow_slow=True, mode=0, stage_b=None):
+def _check(pats, nodes, root, arena, offs, lens, allow_slow=True, mode=0, stage_b=None, per=0):
     """The stream's answers (in-stream fold or stage B) equal the oracle's wherever the
     exact scan is not needed; returns the mask of requests handed to the exact scan (None:
     the ruleset has no stream tables). stage_b: None any, False none may need stage B."""
     hr = H.HostRuleset(pats, nodes, root)
     assert hr.rc == 0, hr.error
-    res = H.eval_stream(hr, arena, offs, lens, mode=mode)
+    res = H.eval_stream(hr, arena, offs, lens, mode=mode, per=per)
     if res is None:
         return None
     tri, err, bm, slow = res
@@ -66,6 +66,16 @@ def test_stream_workloads_match_oracle(wl, n):
     for e in exprs:
         slow = _check(*_flat(e), w.arena, w.offs, w.lens, allow_slow=False)
         assert slow is not None
+
+
+@pytest.mark.parametrize("per", [1, 3, 17])
+def test_stream_fewer_requests_per_wave(per):
+    """The latency configuration: 1..31 requests per wave (small batches spread over more
+    waves) gives the same answers."""
+    from authorino_amd import workloads
+
+    w = workloads.make("c2", n=40, unique=40)
+    assert _check(*_flat(w.expr), w.arena, w.offs, w.lens, allow_slow=False, per=per) is not None
 
 
 def test_stream_every_alignment_and_step_boundary():
