@@ -118,7 +118,8 @@ struct authjx_ctx {
 namespace {
 
 // the last HIP error an entry point returned AUTHJX_EDEVICE for, on this thread
-// (authjx_debug_last_error)
+// (authjx_debug_last_error); the runtime's own last-error slot is cleared, so the caller's
+// next HIP call does not report it again
 thread_local hipError_t t_last_hip = hipSuccess;
 thread_local int t_last_line = 0;
 
@@ -128,6 +129,7 @@ thread_local int t_last_line = 0;
         if (e_ != hipSuccess) {    \
             t_last_hip = e_;       \
             t_last_line = __LINE__; \
+            (void)hipGetLastError(); \
             return AUTHJX_EDEVICE; \
         }                          \
     } while (0)

@@ -372,8 +372,14 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
 // The lean single-pass kernel (ajx_lean.h): stage A with the lean scan, then stage B in the
 // same work-item. Dynamic LDS: [blob copy (SHARED)] [per wave: 64 lanes x 144-B rings].
 constexpr uint32_t kLeanRingBytesPerWave = 64 * lean::kRingStride;
+#ifndef AJX_LEAN_WAVES
+#define AJX_LEAN_WAVES AJX_FAST_WAVES  // waves per SIMD the lean kernel's registers are set for
+#endif
+#ifndef AJX_LEAN_MAXBLOCK
+#define AJX_LEAN_MAXBLOCK kFastMaxBlock
+#endif
 template <bool SHARED>
-__global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_lean(
+__global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_lean(
     const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
     uint64_t* __restrict__ rows, uint32_t row_stride, uint32_t* __restrict__ slow_count,
@@ -417,10 +423,10 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_lean(
 static uint32_t lean_block(uint32_t blob_bytes) {
     const uint32_t stage = (blob_bytes + 15u) & ~15u;
     uint32_t best = 0, best_w = 0;
-    for (uint32_t b = 256; b <= kFastMaxBlock; b *= 2) {
+    for (uint32_t b = 256; b <= AJX_LEAN_MAXBLOCK; b *= 2) {
         const uint32_t lds = stage + (b / 64) * kLeanRingBytesPerWave;
         uint32_t w = lds <= 160u * 1024u ? (160u * 1024u / lds) * (b / 64) : 0u;
-        if (w > 4u * AJX_FAST_WAVES) w = 4u * AJX_FAST_WAVES;
+        if (w > 4u * AJX_LEAN_WAVES) w = 4u * AJX_LEAN_WAVES;
         if (w > best_w) best = b, best_w = w;
     }
     return best ? best : 256u;
@@ -635,7 +641,13 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
                               reinterpret_cast<const void*>(&ajx_scan_stream<0, true>),
                               reinterpret_cast<const void*>(&ajx_stream_finish<false>),
                               reinterpret_cast<const void*>(&ajx_stream_finish<true>)}) {
-            const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            // (the dynamic ceiling is what the kernel's static LDS leaves of the CU's 160 KiB:
+            // stage B's per-thread buffers are static)
+            hipFuncAttributes fa;
+            hipError_t r = hipFuncGetAttributes(&fa, k);
+            if (r != hipSuccess) return r;
+            r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024 - (int)fa.sharedSizeBytes);
             if (r != hipSuccess) return r;
         }
         return hipSuccess;

@@ -502,6 +502,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
     uint32_t req_m = 0, req_v = 0, req_pos = kNone;   // kinds the incoming stack must have
     uint64_t kids = 0;      // key ids by key ordinal in the lane
     uint32_t kbs_ord = 0;   // keys holding a backslash, by key ordinal
+    uint32_t keym = 0;      // keys with an id or a backslash (the only ones the captures look at)
     uint64_t oids = 0;      // container ids by open ordinal
     uint32_t pend_lvl = 0;  // a level opened at byte 0 right after ':' in the lane before
     uint32_t kid31 = 0;     // id of the key whose ':' is byte 31
@@ -560,10 +561,14 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                                 for (uint32_t q = 0; q < klen && !kbs; q++)
                                     kbs = ring[roff + (int32_t)oqpos + 1 + (int32_t)q] == '\\';
                             }
-                            if (kbs) kbs_ord |= 1u << (nk & 31u);
+                            if (kbs) {
+                                kbs_ord |= 1u << (nk & 31u);
+                                keym |= 1u << i;
+                            }
                         }
                     }
                 }
+                if (id) keym |= 1u << i;
                 if (nk < 8) kids |= (uint64_t)id << (8u * nk);
                 nk++;
                 last_kid = id;
@@ -663,13 +668,16 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
         const uint32_t ELQ = T.eg ? CQ & ~Mv & ~((CO >> 1) | (((nx >> 17) & 1u) << 31)) : 0u;
         const uint32_t ELS = T.eg ? SCS & ~nCO : 0u;
         wave::sync();  // (the ring holds every lane's block)
-        if (KEYC | ELQ | ELS) {
+        // the tokens the captures act on: keys with an id (or a backslash), element strings
+        // and scalars, container elements; brackets only up to the last of them
+        const uint32_t OPE = T.eg ? OP & ~nCO : 0u;
+        const uint32_t want = keym | ELQ | ELS | OPE;
+        if (want) {
             const uint32_t ns = T.ns;
             uint64_t* row = rows + (size_t)doc * (1u + ns);
             uint64_t* dec = rows + (size_t)kSpan * (1u + ns) + 4u * doc;
             int32_t dd = depth_in;
             uint64_t iv = (uint64_t)stk_in.iv0 | ((uint64_t)stk_in.iv1 << 32);
-            uint32_t nk = 0, no = 0;
             // the selector whose path is the container at level dd (kNone: none)
             auto container_sel = [&]() -> uint32_t {
                 if (dd < 2 || dd > (int32_t)kStreamMaxComps + 1) return kNone;
@@ -680,20 +688,20 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                 const uint32_t pm = path_meta(T, pth);
                 return (pm && (pm & 0xFFFFu) != 0xFFFFu) ? (pm & 0xFFFFu) : kNone;
             };
-            for (uint32_t m = OP | CL | KEYC | ELQ | ELS; m; m &= m - 1u) {
+            for (uint32_t m = (OP | CL | want) & below(hib(want) + 1u); m; m &= m - 1u) {
                 const uint32_t i = ctz(m);
                 if ((OP >> i) & 1u) {
-                    if (T.eg && !((nCO >> i) & 1u)) {  // a container element: its array is not all strings
+                    if ((OPE >> i) & 1u) {  // a container element: its array is not all strings
                         const uint32_t sa = container_sel();
                         if (sa < 32u) wave::lds_or64(&dec[3], 1ull << sa);
                     }
                     dd++;
+                    const uint32_t no = popc(OP & below(i));  // (the open's ordinal in the lane)
                     if (dd >= 2 && dd <= 9) {
                         const uint32_t sh = 8u * (uint32_t)(dd - 2);
-                        const uint64_t id = (oids >> (8u * no)) & 0xFFu;
+                        const uint64_t id = no < 8 ? (oids >> (8u * no)) & 0xFFu : 0ull;
                         iv = (iv & ~(0xFFull << sh)) | (id << sh);
                     }
-                    no++;
                     continue;
                 }
                 if ((CL >> i) & 1u) {
@@ -730,9 +738,9 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                         wave::lds_or64(&dec[2], (uint64_t)hit << (2u * sa));
                     continue;
                 }
+                const uint32_t nk = popc(KEYC & below(i));  // (the key's ordinal in the lane)
                 const uint32_t own = nk < 8 ? (uint32_t)(kids >> (8u * nk)) & 0xFFu : 0u;
                 const bool kbs = ((kbs_ord >> (nk & 31u)) & 1u) != 0;
-                nk++;
                 if ((!own && !kbs) || dd < 1 || dd > (int32_t)kStreamMaxComps) continue;
                 // the path bytes: the container ids of levels 2..dd, then the key's own id
                 const uint32_t nb = (uint32_t)dd - 1u;

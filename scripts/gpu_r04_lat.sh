@@ -2,7 +2,7 @@
 # c2 at 1M (lean default vs the stream at 32 requests per wave), small batches (stream vs
 # lean), and the c4 serving leg (multi-tenant latency batches on the stream)
 R=$GRAFT_REPO_ROOT; cd $R && O=gpurun_out/${OUT:-r04l} && mkdir -p $O && export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log; grep -E "FAILED|ERROR" $O/pytest.log | head -20
 [ $rc -le 1 ] || { echo "pytest rc=$rc"; exit 1; }
 line() { grep '"metric"' $1 | python3 -c "

@@ -1,0 +1,105 @@
+"""GPU parity of the streaming kernel (authorino_amd/csrc/ajx_stream.h, ajx_scan_stream /
+ajx_stream_finish) against the oracle, through the C-ABI: the bench workloads at 32
+requests per wave (kernel mode 52), small batches at 1..N requests per wave (the default
+path for batches up to the stream threshold), a multi-tenant small batch (one request per
+wave under its own ruleset), mutated and invalid documents (handed to the exact scan:
+results still the oracle's), and the host emulation's decisions on the same inputs
+(tests/test_stream_scan.py) as a cross-check of which requests the stream proves."""
+import numpy as np
+import pytest
+
+import fuzz_util as FU
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from authorino_amd import runtime
+
+    c = runtime.Context(0)
+    yield c
+    c.set_kernel_mode(0)
+    c.set_stream_max(4096)
+
+
+def _pack(docs):
+    lens = np.array([len(d) for d in docs], dtype=np.uint32)
+    offs = np.zeros(len(docs), dtype=np.uint64)
+    if len(docs):
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return np.frombuffer(b"".join(docs) + b"\0" * 64, dtype=np.uint8), offs, lens
+
+
+def _flat(expr):
+    pats, nodes, root = expr.flatten()
+    return [(p.selector, int(p.operator), p.value) for p in pats], nodes, root
+
+
+def _same(ctx, specs, arena, offs, lens, set_of_req=None):
+    sets = [ctx.compile(p, n, r) for p, n, r in specs]
+    tri, err, bm = ctx.eval_host_arena(sets, arena, offs, lens, set_of_req=set_of_req)
+    otri, oerr, obm = O.eval_batch([O.Ruleset(p, n, r) for p, n, r in specs], arena, offs, lens,
+                                   set_of_req=set_of_req, nthreads=8)
+    bad = np.nonzero((tri != otri) | (err != oerr) | (bm[:, :obm.shape[1]] != obm).any(axis=1))[0]
+    assert bad.size == 0, (bad[:10], tri[bad[:10]], otri[bad[:10]], err[bad[:10]], oerr[bad[:10]])
+    return tri
+
+
+@pytest.mark.parametrize("wl,n", [("c2", 20000), ("c5", 3000)])
+def test_stream_workloads_on_device(ctx, wl, n):
+    """The bench documents through the streaming kernel at 32 requests per wave: every
+    request equal to the oracle, none handed to the exact scan."""
+    from authorino_amd import workloads
+
+    w = workloads.make(wl, n=n)
+    exprs = [w.expr] if wl == "c2" else [w.auth_config.conditions] + [
+        e for c in w.auth_config.authorization for e in (c.conditions, c.rules)]
+    ctx.set_kernel_mode(52)
+    try:
+        for e in exprs:
+            _same(ctx, [_flat(e)], w.arena, w.offs, w.lens)
+            assert ctx.last_exact_count() == 0
+    finally:
+        ctx.set_kernel_mode(0)
+
+
+@pytest.mark.parametrize("n", [1, 2, 31, 64, 700, 4096])
+def test_stream_small_batches(ctx, n):
+    """The default path for small batches (requests per wave by batch size)."""
+    from authorino_amd import workloads
+
+    w = workloads.make("c2", n=n, unique=min(n, 256))
+    _same(ctx, [_flat(w.expr)], w.arena, w.offs, w.lens)
+    assert ctx.last_exact_count() == 0
+
+
+def test_stream_multi_tenant_small_batch(ctx):
+    """A small multi-tenant batch: one request per wave, each under its own ruleset."""
+    rng = np.random.default_rng(91)
+    specs = []
+    while len(specs) < 12:
+        pats = FU.rand_patterns(rng, int(rng.integers(1, 6)))
+        if any(part.isdigit() for p in pats for part in p[0].split(".")):
+            continue
+        nodes, root = FU.chain(len(pats))
+        specs.append((pats, nodes, root))
+    docs = [FU.rand_doc(rng, ws=False) for _ in range(600)]
+    sor = np.sort(rng.integers(0, len(specs), len(docs))).astype(np.uint32)
+    _same(ctx, specs, *_pack(docs), set_of_req=sor)
+
+
+def test_stream_mutated_and_invalid_documents(ctx):
+    """Truncated / flipped / whitespace documents and the host tests' invalid list: what the
+    stream does not prove goes to the exact scan, and every result is the oracle's."""
+    from test_stream_scan import INVALID
+
+    rng = np.random.default_rng(92)
+    pats = [("a", 1, "1"), ("b", 2, "v"), ("a.b", 1, "2"), ("a.a.a", 3, "x")]
+    nodes, root = FU.chain(len(pats))
+    docs = list(INVALID) * 3 + [FU.mutate(rng, FU.rand_doc(rng, ws=False)) for _ in range(500)]
+    for n_max in (4096, 0):  # (the stream, then the lean kernel, on the same batch)
+        ctx.set_stream_max(n_max)
+        _same(ctx, [(pats, nodes, root)], *_pack(docs))
+    ctx.set_stream_max(4096)
