@@ -69,7 +69,9 @@ struct Workspace {
     hipEvent_t sets_ev[2] = {nullptr, nullptr};
     bool sets_ev_rec[2] = {false, false};
     std::vector<const uint8_t*> last_sets;
-    uint32_t* d_slow = nullptr;  // [0] = count, [1..] = ids: requests for the exact scan
+    // [0] = count, [1..] = ids: requests for the exact scan (the streaming kernel: [1] its
+    // stage-B count, ids from [2])
+    uint32_t* d_slow = nullptr;
     uint32_t slow_cap = 0;
     uint64_t* d_rows = nullptr;  // stage-A capture rows
     size_t rows_cap = 0;         // in u64
@@ -261,7 +263,7 @@ int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
         if (w->d_slow) (void)hipFree(w->d_slow);
         w->d_slow = nullptr;
         w->slow_cap = 0;
-        HIP_OK(hipMalloc(&w->d_slow, ((size_t)n + 1) * sizeof(uint32_t)));
+        HIP_OK(hipMalloc(&w->d_slow, ((size_t)n + 2) * sizeof(uint32_t)));
         w->slow_cap = n;
     }
     if (n > w->perm_cap) {
@@ -562,7 +564,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         HIP_OK(ajx::launch_eval_stream(w->d_sets, d_set_of_req, (uint32_t)sets[0]->c.blob.size(), max_sel, d_arena,
                                        d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap,
                                        bitmap_stride_words, w->d_rows, rows_stride, keep_rows, w->d_perm, w->d_slow,
-                                       w->d_slow + 1, s, ablate == 50 ? 1 : ablate == 51 ? 2 : 0, mods, per));
+                                       w->d_slow + 2, s, ablate == 50 ? 1 : ablate == 51 ? 2 : 0, mods, per));
     } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
         // caller's bucketing by AuthConfig), a full kernel, batches worth sorting

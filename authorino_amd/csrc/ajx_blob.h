@@ -267,6 +267,10 @@ struct StreamHdr {
     uint32_t n_keys, max_key_len;
     uint32_t light;  // every pattern is an eager one (EagerSel): stage B is the fold alone
     uint32_t pad;
+    // selectors the stream does not follow (an array index, more than kStreamMaxComps
+    // components, a key longer than kStreamMaxKeyLen): stage B takes their values with the
+    // exact Get on the proved document
+    uint32_t exact_lo, exact_hi, pad2[2];
 };
 
 AJX_BLOB_HD inline uint32_t stream_path_hash(uint64_t p, uint32_t log2, uint32_t mult) {

@@ -817,9 +817,18 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         }
         // streaming scan tables (ajx_stream.h): key ids, and the selectors by their
         // component ids
+        // (a selector with an array index, too many components or a long key is left to
+        // stage B's exact Get: the walk below does not enter those edges)
         bool stream_ok = fast_ok && trie[0].selector < 0;
-        for (const Selector& s : sels) stream_ok = stream_ok && s.comp_count <= kStreamMaxComps;
-        for (const Component& c : comps) stream_ok = stream_ok && c.array_index < 0 && c.lit_len <= kStreamMaxKeyLen;
+        uint64_t sexact = 0;
+        for (size_t si = 0; si < sels.size(); si++) {
+            bool ex = sels[si].comp_count > kStreamMaxComps;
+            for (uint32_t k = 0; k < sels[si].comp_count; k++) {
+                const Component& c = comps[sels[si].comp_begin + k];
+                ex = ex || c.array_index >= 0 || c.lit_len > kStreamMaxKeyLen;
+            }
+            if (ex) sexact |= 1ull << si;
+        }
         if (stream_ok) {
             std::map<std::string, uint32_t> key_id;
             std::vector<std::pair<uint64_t, uint32_t>> paths;  // (path bytes, selector)
@@ -829,20 +838,30 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 uint64_t path;
                 uint32_t depth;
             };
+            // an edge the stream follows: a key (not an array index), of at most
+            // kStreamMaxKeyLen bytes, within kStreamMaxComps components
+            auto stream_edge = [&](size_t j, const Walk& w) {
+                return trie[w.node].keys[j].second < 0 && trie[w.node].keys[j].first.size() <= kStreamMaxKeyLen &&
+                       w.depth < kStreamMaxComps;
+            };
             std::vector<Walk> stack{{0u, 0ull, 0u}};
             while (!stack.empty() && stream_ok) {
                 const Walk w = stack.back();
                 stack.pop_back();
-                // (a node's meta: its selector, 0xFFFF none; kStreamHasKids when keys go on below it)
-                if (w.node && (trie[w.node].selector >= 0 || !trie[w.node].kids.empty()))
+                // (a node's meta: its selector, 0xFFFF none; kStreamHasKids when keys the stream
+                // follows go on below it)
+                bool kids = false;
+                for (size_t j = 0; j < trie[w.node].kids.size(); j++) kids = kids || stream_edge(j, w);
+                if (w.node && (trie[w.node].selector >= 0 || kids))
                     paths.push_back({w.path, (trie[w.node].selector >= 0 ? (uint32_t)trie[w.node].selector : 0xFFFFu) |
-                                                 (trie[w.node].kids.empty() ? 0u : kStreamHasKids)});
+                                                 (kids ? kStreamHasKids : 0u)});
                 for (size_t j = 0; j < trie[w.node].kids.size(); j++) {
                     const std::string& key = trie[w.node].keys[j].first;
+                    if (!stream_edge(j, w)) continue;  // (the selectors below: exact Get)
                     auto it = key_id.find(key);
                     if (it == key_id.end()) it = key_id.emplace(key, (uint32_t)key_id.size() + 1).first;
                     max_len = std::max(max_len, (uint32_t)key.size());
-                    if (it->second > kStreamMaxKeys || w.depth >= kStreamMaxComps) {
+                    if (it->second > kStreamMaxKeys) {
                         stream_ok = false;
                         break;
                     }
@@ -922,7 +941,9 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                             (pt.op == OP_EQ || pt.op == OP_NEQ || pt.op == OP_INCL || pt.op == OP_EXCL);
                 }
                 for (size_t sidx = 0; sidx < sel_pats.size() && light; sidx++) light = sel_pats[sidx].size() <= 2;
-                sh.light = light ? 1u : 0u;
+                sh.light = light && !sexact ? 1u : 0u;
+                sh.exact_lo = (uint32_t)sexact;
+                sh.exact_hi = (uint32_t)(sexact >> 32);
                 hdr.off_stream = (uint32_t)b.align16();
                 b.append(&sh, sizeof sh);
                 StreamHdr* shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);

@@ -510,6 +510,9 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
     }
 }
 
+// a stage-B list entry the stream could not prove (merge_slow): the exact scan decides it
+constexpr uint32_t kStageExact = 1u << 31;
+
 // The streaming kernel (ajx_stream.h): each wave takes a span of stream::kSpan requests in
 // arena order and reads their bytes as one coalesced stream; a lane per request then folds
 // the patterns the stream decided. Requests with a pattern left (a value to parse or
@@ -529,11 +532,12 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
                                                        const uint64_t* __restrict__ offs,
                                                        const uint32_t* __restrict__ lens, uint32_t n,
                                                        uint32_t* __restrict__ slow_count,
-                                                       uint32_t* __restrict__ slow_ids, uint32_t* __restrict__ stage_list,
+                                                       uint32_t* __restrict__ slow_ids, uint32_t* __restrict__ stage_ids,
                                                        uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
                                                        uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t wave_off,
                                                        uint32_t wave_bytes, uint64_t* __restrict__ rows_out,
-                                                       uint32_t row_stride, uint32_t keep_rows, uint32_t per) {
+                                                       uint32_t row_stride, uint32_t keep_rows, uint32_t per,
+                                                       uint32_t merge_slow) {
     extern __shared__ uint4 s_stream_dyn[];
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
     const uint32_t span = blockIdx.x * (blockDim.x >> 6) + w;
@@ -555,7 +559,13 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
     if (l >= per || r >= n || MODE != 0) return;
     const RowRef o = wave_row(rows_out, row_stride, r);
     if (res == stream::R_SLOW) {
-        slow_ids[atomicAdd(slow_count, 1u)] = r;
+        // (merge_slow: the stage-B kernel runs its exact scan, flagged on the stage-B list)
+        if (merge_slow) {
+            atomicAdd(slow_count, 1u);
+            stage_ids[atomicAdd(slow_count + 1, 1u)] = r | kStageExact;
+        } else {
+            slow_ids[atomicAdd(slow_count, 1u)] = r;
+        }
         if (keep_rows) o[0] = kRowSlow;
         return;
     }
@@ -566,7 +576,7 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
     if (res == stream::R_STAGE_B || open) {
         for (uint32_t s = 0; s <= ns; s++) o[s] = rowp[s];
         for (uint32_t k = 0; k < 4; k++) o[1u + ns + k] = dwp[k];
-        stage_list[1u + atomicAdd(stage_list, 1u)] = r;
+        stage_ids[atomicAdd(slow_count + 1, 1u)] = r;  // (the stage-B count follows the slow count)
     } else if (keep_rows) {
         for (uint32_t s = 0; s <= ns; s++) o[s] = rowp[s];
     }
@@ -574,27 +584,44 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
 
 // Stage B of the streaming kernel: one work-item per request on the stage-B list, on its
 // row in HBM (stream::finish_full); what it can not decide goes to the slow list. MT: each
-// request's own ruleset, read from global memory.
-template <bool MT = false>
+// request's own ruleset, read from global memory. EXACT (small batches, one launch fewer):
+// the exact scan runs here, for the requests the stream flagged (kStageExact) and for those
+// stage B can not decide; 1 without, 2 with modifier buffers.
+template <bool MT = false, int EXACT = 0>
 __global__ __launch_bounds__(256) void ajx_stream_finish(const uint8_t* const* __restrict__ sets,
                                                          const uint32_t* __restrict__ set_of_req,
                                                          const uint8_t* __restrict__ arena,
                                                          const uint64_t* __restrict__ offs,
                                                          const uint32_t* __restrict__ lens,
-                                                         const uint32_t* __restrict__ stage_list,
+                                                         const uint32_t* __restrict__ stage_ids,
                                                          uint64_t* __restrict__ rows, uint32_t row_stride,
                                                          uint32_t* __restrict__ slow_count,
                                                          uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri,
                                                          int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
                                                          uint32_t stride) {
     const uint8_t* blob0 = MT ? nullptr : stage_blob<true>(sets[0]);
-    const uint32_t cnt = *stage_list;
+    const uint32_t cnt = slow_count[1];  // (the stage-B count)
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
-        const uint32_t r = stage_list[1u + i];
+        const uint32_t e = stage_ids[i];
+        const uint32_t r = e & ~kStageExact;
         const uint8_t* blob = MT ? sets[set_of_req[r]] : blob0;
-        if (!stream::finish_full(r, blob, arena + offs[r], lens[r], wave_row(rows, row_stride, r), out_tri, out_err,
-                                 out_bm, stride))
+        bool ok = false;
+        if (!(e & kStageExact))
+            ok = stream::finish_full(r, blob, arena + offs[r], lens[r], wave_row(rows, row_stride, r), out_tri,
+                                     out_err, out_bm, stride);
+        if (ok) continue;
+        if constexpr (EXACT == 0) {
             slow_ids[atomicAdd(slow_count, 1u)] = r;
+        } else {
+            if (!(e & kStageExact)) atomicAdd(slow_count, 1u);
+            if constexpr (EXACT == 2) {
+                ModBufs mb;
+                eval_scan_one<true>(r, sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride, &mb);
+            } else {
+                eval_scan_one<false>(r, sets, set_of_req, arena, offs, lens, out_tri, out_err, out_bm, stride,
+                                     nullptr);
+            }
+        }
     }
 }
 
@@ -612,7 +639,7 @@ constexpr uint32_t kStreamBlock = 256;
 hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t blob_bytes,
                               uint32_t n_selectors, const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                               uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
-                              uint32_t row_stride, bool keep_rows, uint32_t* d_stage_list, uint32_t* d_slow_count,
+                              uint32_t row_stride, bool keep_rows, uint32_t* d_stage_ids, uint32_t* d_slow_count,
                               uint32_t* d_slow_ids, hipStream_t stream, int mode, bool mods, uint32_t per) {
     if (n == 0) return hipSuccess;
     if (row_stride < 5u + n_selectors) return hipErrorInvalidValue;
@@ -628,11 +655,14 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
     const uint32_t lds = wave_off + (block / 64) * wave_bytes;
     if (lds > 160u * 1024u) return hipErrorInvalidValue;
     if (per == 0 || per > stream::kSpan) per = stream::kSpan;
+    // a small batch (fewer requests per wave, or one per wave under its own ruleset): stage B
+    // runs the exact scan too (one launch fewer on the latency path)
+    const bool merge = mt || per < stream::kSpan;
     const uint32_t spans = (n + per - 1) / per;
     const uint32_t grid = (spans + block / 64 - 1) / (block / 64);
-    hipError_t e = hipMemsetAsync(d_slow_count, 0, sizeof(uint32_t), stream);
+    // (one fill: the slow count and the stage-B count after it)
+    hipError_t e = hipMemsetAsync(d_slow_count, 0, 2 * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(d_stage_list, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
     static std::atomic<uint64_t> attr_done{0};
     e = attr_once(attr_done, [] {
         for (const void* k : {reinterpret_cast<const void*>(&ajx_scan_stream<0>),
@@ -640,7 +670,10 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
                               reinterpret_cast<const void*>(&ajx_scan_stream<2>),
                               reinterpret_cast<const void*>(&ajx_scan_stream<0, true>),
                               reinterpret_cast<const void*>(&ajx_stream_finish<false>),
-                              reinterpret_cast<const void*>(&ajx_stream_finish<true>)}) {
+                              reinterpret_cast<const void*>(&ajx_stream_finish<false, 1>),
+                              reinterpret_cast<const void*>(&ajx_stream_finish<false, 2>),
+                              reinterpret_cast<const void*>(&ajx_stream_finish<true, 1>),
+                              reinterpret_cast<const void*>(&ajx_stream_finish<true, 2>)}) {
             // (the dynamic ceiling is what the kernel's static LDS leaves of the CU's 160 KiB:
             // stage B's per-thread buffers are static)
             hipFuncAttributes fa;
@@ -656,8 +689,8 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
 #define AJX_STREAM_LAUNCH(M, T)                                                                               \
     hipLaunchKernelGGL((ajx_scan_stream<M, T>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena, \
                        d_offs, d_lens, n, \
-                       d_slow_count, d_slow_ids, d_stage_list, d_tri, d_err, d_bm, stride, wave_off, wave_bytes,      \
-                       d_rows, row_stride, keep_rows ? 1u : 0u, per)
+                       d_slow_count, d_slow_ids, d_stage_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes,       \
+                       d_rows, row_stride, keep_rows ? 1u : 0u, per, merge ? 1u : 0u)
     if (mt)
         AJX_STREAM_LAUNCH(0, true);
     else if (mode == 1)
@@ -671,15 +704,23 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
     if (mode != 0) return hipSuccess;
     // stage B and the exact scan over their lists (grid-stride: the lists' lengths are on the device)
     const uint32_t fgrid = n < 2048u * 256u ? (n + 255) / 256 : 4096;
-    if (mt)
-        hipLaunchKernelGGL(ajx_stream_finish<true>, dim3(fgrid), dim3(256), 0, stream, d_sets, d_set_of_req, d_arena,
-                           d_offs, d_lens, d_stage_list, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
-                           d_bm, stride);
+#define AJX_FINISH_LAUNCH(T, X, LDS)                                                                              \
+    hipLaunchKernelGGL((ajx_stream_finish<T, X>), dim3(fgrid), dim3(256), LDS, stream, d_sets,                    \
+                       T ? d_set_of_req : nullptr, d_arena, d_offs, d_lens, d_stage_ids, d_rows, row_stride,      \
+                       d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride)
+    if (mt && mods)
+        AJX_FINISH_LAUNCH(true, 2, 0);
+    else if (mt)
+        AJX_FINISH_LAUNCH(true, 1, 0);
+    else if (merge && mods)
+        AJX_FINISH_LAUNCH(false, 2, wave_off);
+    else if (merge)
+        AJX_FINISH_LAUNCH(false, 1, wave_off);
     else
-        hipLaunchKernelGGL(ajx_stream_finish<false>, dim3(fgrid), dim3(256), wave_off, stream, d_sets, nullptr,
-                           d_arena, d_offs, d_lens, d_stage_list, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri,
-                           d_err, d_bm, stride);
+        AJX_FINISH_LAUNCH(false, 0, wave_off);
+#undef AJX_FINISH_LAUNCH
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (merge) return hipSuccess;
     const uint32_t sgrid = n < 1024u * 128u ? 2 * ((n + 255) / 256) : 4096;
     launch_slow_list(mods, sgrid, stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, d_slow_count, d_slow_ids, d_tri,
                      d_err, d_bm, stride);

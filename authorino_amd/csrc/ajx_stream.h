@@ -185,6 +185,7 @@ struct Tabs {
     const EagerSel* eg;  // (null: none)
     const uint8_t* lits;
     uint32_t k_log2, k_mult, k_probes, p_log2, p_mult, p_probes, max_key_len, ns;
+    uint32_t exact;  // some selector takes the exact Get in stage B (StreamHdr exact_lo / hi)
 };
 AJX_HD Tabs tabs_of(const uint8_t* blob) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
@@ -202,6 +203,7 @@ AJX_HD Tabs tabs_of(const uint8_t* blob) {
     t.p_probes = lean::uni(s->path_probes);
     t.max_key_len = lean::uni(s->max_key_len);
     t.ns = lean::uni(h->n_selectors);
+    t.exact = lean::uni(s->exact_lo | s->exact_hi);
     return t;
 }
 
@@ -941,7 +943,7 @@ AJX_HD bool finish_light(uint32_t r, const uint8_t* blob, const Tabs& T, const u
                          uint32_t stride) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const uint32_t np = h->n_patterns;
-    if (np > 64 || (h->static_error[0] | h->unsupported[0])) return false;
+    if (np > 64 || (h->static_error[0] | h->unsupported[0]) || T.exact) return false;
     uint64_t dD = dw[0], dT = dw[1];
     array_decisions(T.eg, T.ns, RowRef(row), dw, dD, dT);
     const SelectorPatterns* sps = reinterpret_cast<const SelectorPatterns*>(blob + h->off_sel_patterns);
@@ -989,6 +991,23 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
     const uint64_t dw[4] = {row[1u + ns], row[2u + ns], row[3u + ns], row[4u + ns]};
     uint64_t dD = dw[0], dT = dw[1];
     array_decisions(eg, ns, row, dw, dD, dT);
+    // the selectors the stream does not follow: the exact Get on the proved document
+    const StreamHdr* sh = reinterpret_cast<const StreamHdr*>(blob + h->off_stream);
+    const uint64_t exact = (uint64_t)sh->exact_lo | ((uint64_t)sh->exact_hi << 32);
+    if (exact) {
+        const Selector* sels = reinterpret_cast<const Selector*>(blob + h->off_selectors);
+        const Component* comps = reinterpret_cast<const Component*>(blob + h->off_components);
+        const uint8_t* lits = blob + h->off_literals;
+        for (uint64_t m = exact; m; m &= m - 1ull) {
+            const uint32_t s = (uint32_t)__builtin_ctzll(m);
+            const ValueRef v = gj_get(d, n, comps + sels[s].comp_begin, sels[s].comp_count, lits);
+            if (v.type == T_NULL && v.start == v.end) continue;  // (not found: Null)
+            row[1u + s] = (uint64_t)v.start |
+                          ((uint64_t)(((v.end - v.start) & 0xFFFFFFu) | ((uint32_t)v.type << 24) |
+                                      ((uint32_t)(v.esc & 1u) << 27)) << 32);
+            row[0] = row[0] | (1ull << s);
+        }
+    }
     for (uint32_t s = 0; s < ns; s++) {
         uint64_t rec = row[1u + s];
         if ((uint32_t)rec == kNone || !((rec >> 32) & kOpenEnd)) continue;

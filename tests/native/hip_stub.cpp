@@ -125,10 +125,11 @@ bool stream_eligible(const uint8_t*, uint32_t) { return true; }
 hipError_t launch_eval_stream(const uint8_t* const*, const uint32_t*, uint32_t, uint32_t, const uint8_t*,
                               const uint64_t*, const uint32_t*, uint32_t n, uint8_t* tri, int32_t* err, uint64_t* bm,
                               uint32_t stride, uint64_t* rows, uint32_t row_stride, bool keep_rows,
-                              uint32_t* stage_list, uint32_t* slow_count, uint32_t*, hipStream_t, int, bool,
+                              uint32_t* stage_ids, uint32_t* slow_count, uint32_t*, hipStream_t, int, bool,
                               uint32_t) {
-    *slow_count = n / 5;
-    stage_list[0] = 0;
+    slow_count[0] = n / 5;
+    slow_count[1] = 0;
+    (void)stage_ids;
     if (keep_rows)
         for (uint32_t r = 0; r < n; r++) rows[(size_t)r * row_stride] = r;
     results(n, tri, err, bm, stride);

@@ -79,15 +79,31 @@ def test_stream_multi_tenant_small_batch(ctx):
     """A small multi-tenant batch: one request per wave, each under its own ruleset."""
     rng = np.random.default_rng(91)
     specs = []
-    while len(specs) < 12:
+    while len(specs) < 12:  # (array indices included: stage B's exact Get)
         pats = FU.rand_patterns(rng, int(rng.integers(1, 6)))
-        if any(part.isdigit() for p in pats for part in p[0].split(".")):
-            continue
         nodes, root = FU.chain(len(pats))
         specs.append((pats, nodes, root))
     docs = [FU.rand_doc(rng, ws=False) for _ in range(600)]
     sor = np.sort(rng.integers(0, len(specs), len(docs))).astype(np.uint32)
     _same(ctx, specs, *_pack(docs), set_of_req=sor)
+
+
+def test_stream_c4_small_multi_tenant_batches(ctx):
+    """c4's AuthConfigs (array-index selectors among them) in small multi-tenant batches,
+    as the micro-batcher sends them: one request per wave, equal to the oracle."""
+    from authorino_amd import workloads
+
+    w = workloads.make("c4", n=3000)
+    specs = [_flat(e) for e in w.exprs]
+    used = sorted(set(int(x) for x in w.set_of_req[:3000]))
+    remap = {u: i for i, u in enumerate(used)}
+    sor = np.array([remap[int(x)] for x in w.set_of_req[:3000]], dtype=np.uint32)
+    for lo in range(0, 3000, 1000):
+        hi = lo + 1000
+        sub = sorted(set(sor[lo:hi].tolist()))
+        m = {u: i for i, u in enumerate(sub)}
+        _same(ctx, [specs[used[u]] for u in sub], w.arena, w.offs[lo:hi], w.lens[lo:hi],
+              set_of_req=np.array([m[int(x)] for x in sor[lo:hi]], dtype=np.uint32))
 
 
 def test_stream_mutated_and_invalid_documents(ctx):
