@@ -525,7 +525,10 @@ constexpr uint32_t kStageExact = 1u << 31;
 // Dynamic LDS: [blob copy] [per wave: WaveLds, capture rows, eager decisions].
 // MT (multi-tenant latency batches): one request per wave (per = 1) under its own
 // ruleset sets[set_of_req[r]], its tables read from global memory (L2), no blob copy.
-template <int MODE, bool MT = false>
+// LAT (small batches, no kept rows): a span that fit one step has its documents in LDS
+// still, and its lanes run stage B there (finish_full on the ring); what that leaves goes
+// to the exact scan through the stage-B list.
+template <int MODE, bool MT = false, bool LAT = false>
 __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __restrict__ sets,
                                                        const uint32_t* __restrict__ set_of_req,
                                                        const uint8_t* __restrict__ arena,
@@ -553,10 +556,21 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
     uint64_t* rows = reinterpret_cast<uint64_t*>(base + sizeof(stream::WaveLds));
     if (span * per >= n) return;  // (wave-uniform)
     const uint64_t *rowp = nullptr, *dwp = nullptr;
+    const uint8_t* lds_doc = nullptr;
     const uint32_t res = stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
-                                                 out_bm, stride, &rowp, &dwp);
+                                                 out_bm, stride, &rowp, &dwp, LAT ? &lds_doc : nullptr);
     const uint32_t r = span * per + l;
     if (l >= per || r >= n || MODE != 0) return;
+    if constexpr (LAT) {
+        if (res == stream::R_STAGE_B && lds_doc) {
+            if (!stream::finish_full(r, blob, lds_doc, lens[r], RowRef(rowp), out_tri, out_err, out_bm, stride,
+                                     dwp)) {
+                atomicAdd(slow_count, 1u);
+                stage_ids[atomicAdd(slow_count + 1, 1u)] = r | kStageExact;
+            }
+            return;
+        }
+    }
     const RowRef o = wave_row(rows_out, row_stride, r);
     if (res == stream::R_SLOW) {
         // (merge_slow: the stage-B kernel runs its exact scan, flagged on the stage-B list)
@@ -669,6 +683,8 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
                               reinterpret_cast<const void*>(&ajx_scan_stream<1>),
                               reinterpret_cast<const void*>(&ajx_scan_stream<2>),
                               reinterpret_cast<const void*>(&ajx_scan_stream<0, true>),
+                              reinterpret_cast<const void*>(&ajx_scan_stream<0, false, true>),
+                              reinterpret_cast<const void*>(&ajx_scan_stream<0, true, true>),
                               reinterpret_cast<const void*>(&ajx_stream_finish<false>),
                               reinterpret_cast<const void*>(&ajx_stream_finish<false, 1>),
                               reinterpret_cast<const void*>(&ajx_stream_finish<false, 2>),
@@ -686,19 +702,25 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
         return hipSuccess;
     });
     if (e != hipSuccess) return e;
-#define AJX_STREAM_LAUNCH(M, T)                                                                               \
-    hipLaunchKernelGGL((ajx_scan_stream<M, T>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req, d_arena, \
+#define AJX_STREAM_LAUNCH(M, T, LT)                                                                           \
+    hipLaunchKernelGGL((ajx_scan_stream<M, T, LT>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,     \
+                       d_arena, \
                        d_offs, d_lens, n, \
                        d_slow_count, d_slow_ids, d_stage_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes,       \
                        d_rows, row_stride, keep_rows ? 1u : 0u, per, merge ? 1u : 0u)
-    if (mt)
-        AJX_STREAM_LAUNCH(0, true);
+    const bool lat = merge && !keep_rows;
+    if (mt && lat)
+        AJX_STREAM_LAUNCH(0, true, true);
+    else if (mt)
+        AJX_STREAM_LAUNCH(0, true, false);
     else if (mode == 1)
-        AJX_STREAM_LAUNCH(1, false);
+        AJX_STREAM_LAUNCH(1, false, false);
     else if (mode == 2)
-        AJX_STREAM_LAUNCH(2, false);
+        AJX_STREAM_LAUNCH(2, false, false);
+    else if (lat)
+        AJX_STREAM_LAUNCH(0, false, true);
     else
-        AJX_STREAM_LAUNCH(0, false);
+        AJX_STREAM_LAUNCH(0, false, false);
 #undef AJX_STREAM_LAUNCH
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mode != 0) return hipSuccess;

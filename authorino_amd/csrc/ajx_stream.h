@@ -868,12 +868,28 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
 // valid compact JSON. false: a literal gjson would read differently (exact scan).
 AJX_HD bool resolve_open(const uint8_t* d, uint32_t n, uint32_t a, uint64_t* rec) {
     if (a >= n) return false;
-    const uint32_t b0 = d[a];
+    // the bytes come through one aligned 16-byte block at a time (a byte loop of global
+    // loads would pay a load latency per byte)
+    const V4* dq = reinterpret_cast<const V4*>((uintptr_t)d & ~(uintptr_t)15);
+    const uint32_t dm = (uint32_t)((uintptr_t)d & 15u);
+    uint32_t qi = 0xFFFFFFFFu;
+    V4 q{0u, 0u, 0u, 0u};
+    auto byte = [&](uint32_t i) -> uint32_t {
+        const uint32_t g = i + dm;
+        if ((g >> 4) != qi) {
+            qi = g >> 4;
+            q = dq[qi];
+        }
+        const uint32_t w = (g >> 2) & 3u;
+        const uint32_t v = w == 0 ? q.x : w == 1 ? q.y : w == 2 ? q.z : q.w;
+        return (v >> (8u * (g & 3u))) & 0xFFu;
+    };
+    const uint32_t b0 = byte(a);
     uint32_t type, end = a + 1u, esc = 0;
     if (b0 == '"') {
         type = T_STRING;
-        while (end < n && d[end] != '"') {
-            if (d[end] == '\\') {
+        while (end < n && byte(end) != '"') {
+            if (byte(end) == '\\') {
                 esc = 1;
                 end++;
             }
@@ -884,10 +900,10 @@ AJX_HD bool resolve_open(const uint8_t* d, uint32_t n, uint32_t a, uint64_t* rec
         type = T_JSON;
         uint32_t depth = 1;
         while (end < n && depth) {
-            const uint32_t ch = d[end];
+            const uint32_t ch = byte(end);
             if (ch == '"') {
                 end++;
-                while (end < n && d[end] != '"') end += d[end] == '\\' ? 2u : 1u;
+                while (end < n && byte(end) != '"') end += byte(end) == '\\' ? 2u : 1u;
             } else if (ch == '{' || ch == '[') {
                 depth++;
             } else if (ch == '}' || ch == ']') {
@@ -897,15 +913,15 @@ AJX_HD bool resolve_open(const uint8_t* d, uint32_t n, uint32_t a, uint64_t* rec
         }
     } else {
         type = T_NUMBER;
-        while (end < n && d[end] != ',' && d[end] != '}' && d[end] != ']') {
-            if (d[end] <= ' ') return false;  // (gjson's scalar would end there)
+        while (end < n && byte(end) != ',' && byte(end) != '}' && byte(end) != ']') {
+            if (byte(end) <= ' ') return false;  // (gjson's scalar would end there)
             end++;
         }
         const uint32_t k = end - a;
         if (b0 == 't' || b0 == 'f' || b0 == 'n') {  // literals must be exact (as the stream's)
-            const bool t = b0 == 't' && k == 4 && d[a + 1] == 'r' && d[a + 2] == 'u' && d[a + 3] == 'e';
-            const bool f = b0 == 'f' && k == 5 && d[a + 1] == 'a' && d[a + 2] == 'l' && d[a + 3] == 's' && d[a + 4] == 'e';
-            const bool z = b0 == 'n' && k == 4 && d[a + 1] == 'u' && d[a + 2] == 'l' && d[a + 3] == 'l';
+            const bool t = b0 == 't' && k == 4 && byte(a + 1) == 'r' && byte(a + 2) == 'u' && byte(a + 3) == 'e';
+            const bool f = b0 == 'f' && k == 5 && byte(a + 1) == 'a' && byte(a + 2) == 'l' && byte(a + 3) == 's' && byte(a + 4) == 'e';
+            const bool z = b0 == 'n' && k == 4 && byte(a + 1) == 'u' && byte(a + 2) == 'l' && byte(a + 3) == 'l';
             if (!(t || f || z)) return false;
             type = t ? T_TRUE : f ? T_FALSE : T_NULL;
         }
@@ -982,13 +998,15 @@ AJX_HD bool finish_light(uint32_t r, const uint8_t* blob, const Tabs& T, const u
 // request; its row in HBM: found word, records, the 4 eager words): the open values from
 // the document, the arrays' decisions, ajx_fast.h's patterns_from_row, the T bitmap and the
 // fold. false: the exact scan decides the request (the row is marked kRowSlow).
+// dwp: the eager words (null: they follow the row's records, as in the stage-B rows).
 AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint32_t n, RowRef row,
                         uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
-                        uint32_t stride) {
+                        uint32_t stride, const uint64_t* dwp = nullptr) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const uint32_t ns = h->n_selectors;
     const EagerSel* eg = h->off_eager ? reinterpret_cast<const EagerSel*>(blob + h->off_eager) : nullptr;
-    const uint64_t dw[4] = {row[1u + ns], row[2u + ns], row[3u + ns], row[4u + ns]};
+    const uint64_t dw[4] = {dwp ? dwp[0] : row[1u + ns], dwp ? dwp[1] : row[2u + ns], dwp ? dwp[2] : row[3u + ns],
+                            dwp ? dwp[3] : row[4u + ns]};
     uint64_t dD = dw[0], dT = dw[1];
     array_decisions(eg, ns, row, dw, dD, dT);
     // the selectors the stream does not follow: the exact Get on the proved document
@@ -1008,9 +1026,13 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
             row[0] = row[0] | (1ull << s);
         }
     }
+    const SelectorPatterns* sps = reinterpret_cast<const SelectorPatterns*>(blob + h->off_sel_patterns);
     for (uint32_t s = 0; s < ns; s++) {
         uint64_t rec = row[1u + s];
         if ((uint32_t)rec == kNone || !((rec >> 32) & kOpenEnd)) continue;
+        // (every pattern of the selector decided already: its value is not read; a forest's
+        // rows are kept for authjx_select_from_eval_device, whose values must all be closed)
+        if (!h->pad1[0] && !(sps[s].mask[0] & ~dD) && !sps[s].mask[1]) continue;
         if (!resolve_open(d, n, (uint32_t)rec, &rec)) {
             row[0] = kRowSlow;
             return false;
@@ -1059,7 +1081,7 @@ AJX_HD uint32_t scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const
                           const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
                           uint32_t span, uint32_t per, uint32_t l, uint8_t* __restrict__ out_tri,
                           int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm, uint32_t stride,
-                          const uint64_t** row_out, const uint64_t** dw_out) {
+                          const uint64_t** row_out, const uint64_t** dw_out, const uint8_t** lds_doc = nullptr) {
     const Tabs T = tabs_of(blob);
     const uint32_t r = span * per + l;
     const bool my = l < per && r < n;
@@ -1092,6 +1114,12 @@ AJX_HD uint32_t scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const
     }
     const bool proved = L.root_end[l] != kNone && L.bad[l] > L.root_end[l];
     if (!proved) return R_SLOW;
+    // (a span of one step: its documents are still in the ring, at ring index 64 + their
+    // stream byte address)
+    if (lds_doc && nsteps == 1) {
+        const DocEnt e = L.doc[l];
+        *lds_doc = L.ring_raw + 16 + 64 + e.start * 32u + (e.len_mis >> 24);
+    }
     uint64_t* row = rows + (size_t)l * (1u + T.ns);
     const uint64_t* dp = rows + (size_t)kSpan * (1u + T.ns) + 4u * l;
     *row_out = row;

@@ -345,18 +345,27 @@ extern "C" int ht_eval_stream(void* h, const uint8_t* arena, const uint64_t* off
         stream::WaveLds& L = *reinterpret_cast<stream::WaveLds*>(wl.data());
         uint64_t* rows = wl.data() + sizeof(stream::WaveLds) / 8;
         std::mutex mu;
+        // (as the kernel's LAT instance for small batches: per < 32)
+        const bool lat = per < stream::kSpan;
         wave::run_wave([&](uint32_t l) {
             const uint64_t *rowp = nullptr, *dwp = nullptr;
+            const uint8_t* lds_doc = nullptr;
             uint32_t res;
             if (mode == 1)
                 res = stream::scan_span<1>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
                                            out_bm, stride, &rowp, &dwp);
             else
                 res = stream::scan_span<0>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
-                                           out_bm, stride, &rowp, &dwp);
+                                           out_bm, stride, &rowp, &dwp, lat ? &lds_doc : nullptr);
             const uint32_t r = span * per + l;
             if (l >= per || r >= n) return;
             out_slow[r] = res == stream::R_SLOW ? 1 : 0;
+            if (res == stream::R_STAGE_B && lds_doc) {  // stage B on the ring's copy of the document
+                const bool ok = stream::finish_full(r, blob, lds_doc, lens[r], RowRef(const_cast<uint64_t*>(rowp)),
+                                                    out_tri, out_err, out_bm, stride, dwp);
+                out_slow[r] = ok ? 2 : 1;
+                return;
+            }
             if (res == stream::R_STAGE_B) {
                 uint64_t* o = stage_rows.data() + (size_t)r * (5 + ns);
                 std::memcpy(o, rowp, (1 + ns) * 8);

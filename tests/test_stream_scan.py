@@ -103,6 +103,18 @@ def _stream_patterns(rng, k):
     return FU.rand_patterns(rng, k)  # (array indices: stage B's exact Get)
 
 
+@pytest.mark.parametrize("per", [1, 4])
+def test_stream_small_batch_stage_b_in_lds(per):
+    """Small batches: spans that fit one step run stage B on the ring's copy of each document
+    (the kernel's LAT instance), array-index selectors included (exact Get on the copy)."""
+    rng = np.random.default_rng(600 + per)
+    for _ in range(4):
+        pats = _stream_patterns(rng, int(rng.integers(1, 7)))
+        nodes, root = FU.chain(len(pats))
+        docs = [FU.rand_doc(rng, ws=False) for _ in range(48)]
+        _check(pats, nodes, root, *_pack(docs), per=per)
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_stream_random_documents(seed):
     """Random compact documents and selectors: bit-exact where decided (light and full
