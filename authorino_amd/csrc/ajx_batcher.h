@@ -133,9 +133,11 @@ class BatchCore {
                 std::unique_lock<std::mutex> lock(mu_);
                 cv_work_.wait(lock, [&] { return stopping_ || !q_.empty(); });
                 if (q_.empty()) return;  // stopping, nothing left
-                // a full batch or the oldest request's window, whichever comes first
-                const uint64_t flush_at = q_.front()->enq_ns + window_ns_;
-                while (!stopping_ && q_.size() < max_batch_) {
+                // a full batch or the oldest request's window, whichever comes first (the
+                // oldest is looked up after every wake: another worker may have taken the
+                // requests this one was waiting for, and newer ones get their own window)
+                while (!stopping_ && !q_.empty() && q_.size() < max_batch_) {
+                    const uint64_t flush_at = q_.front()->enq_ns + window_ns_;
                     const uint64_t now = mono_ns();
                     if (now >= flush_at) break;
                     cv_work_.wait_for(lock, std::chrono::nanoseconds(flush_at - now));

@@ -221,7 +221,7 @@ struct RulesetHdr {
 };
 constexpr uint32_t kFlagFastOk = 4;
 
-constexpr uint32_t kFlagBufs = 8;
+constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the exact scan's buffers
 
 // Patterns the lean scan decides while it captures (ajx_lean.h): per selector, its first
 // two patterns (index < 64) that compare an unescaped string value's text with a literal
@@ -233,7 +233,7 @@ struct EagerSel {
     uint32_t pad[2];
 };
 static_assert(sizeof(EagerSel) == 48, "EagerSel layout");
-constexpr uint32_t kEagerValid = 1u << 31;  // a selector builds a text (a '#' list): the exact scan's buffers
+constexpr uint32_t kEagerValid = 1u << 31;  // EagerSel::m[k] holds an eager pattern
 
 // ---- streaming scan (ajx_stream.h) ------------------------------------------------
 // The stream resolves object keys without their parent: every distinct object key of the

@@ -456,8 +456,9 @@ def main():
         # serving goroutines would (main.go:69,451; pkg/service/auth_pipeline.go:150-164)
         extra["serving"] = []
         # (64 producers: the VERDICT's case; 256: a loaded server, within the box's task cap;
-        # the window trades latency for batch size)
-        for threads, window_us in ((64, 200), (64, 50), (256, 200)):
+        # the window trades latency for batch size; batches up to the stream threshold take
+        # the streaming kernel, one request per wave)
+        for threads, window_us in ((64, 200), (64, 50), (64, 20), (256, 200)):
             ns = min(w.n, 1 << 18)
             b = runtime.Batcher(ctx, max_batch=8192, window_us=window_us)
             try:

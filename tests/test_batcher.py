@@ -122,3 +122,28 @@ def test_queue_room_wait_honours_the_deadline(lib):
         t.join()
     lib.hb_destroy(h)
     assert rcs.count(ETIMEDOUT) >= 8 and rcs.count(0) >= 1
+
+
+def test_two_workers_keep_each_requests_window(lib):
+    """with two workers, a worker that wakes after the other one drained the queue
+    waits for the NEW oldest request's window (it used to flush at the old deadline, sending
+    small batches early). 16 closed-loop producers and a 3 ms window: batches stay full."""
+    h = lib.hb_create(64, 3000, 0, 300)
+    done = []
+
+    def producer(seed):
+        out = (C.c_uint8 * 1)()
+        for i in range(40):
+            assert lib.hb_eval(h, 1 + (seed % 3), 1, (seed + i) & 0xFF, 0, out) == 0
+        done.append(seed)
+
+    ts = [threading.Thread(target=producer, args=(s,)) for s in range(16)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    st = _stats(lib, h)
+    lib.hb_destroy(h)
+    assert len(done) == 16 and st["requests"] == 16 * 40
+    print(st)
+    assert st["requests"] / st["batches"] >= 12, st  # (mean batch size; 16 would be ideal)
