@@ -156,6 +156,19 @@ AJX_HD uint32_t hexval4(const uint8_t* s) {
     return v;
 }
 
+// the same UTF-8 bytes packed low byte first into *w (register-resident: no byte array)
+AJX_HD uint32_t utf8_put32(uint32_t r, uint32_t* w) {
+    if (r > 0x10FFFF || (r >= 0xD800 && r <= 0xDFFF)) r = 0xFFFD;
+    if (r < 0x80) { *w = r; return 1; }
+    if (r < 0x800) { *w = (0xC0 | (r >> 6)) | ((0x80 | (r & 0x3F)) << 8); return 2; }
+    if (r < 0x10000) {
+        *w = (0xE0 | (r >> 12)) | ((0x80 | ((r >> 6) & 0x3F)) << 8) | ((0x80 | (r & 0x3F)) << 16);
+        return 3;
+    }
+    *w = (0xF0 | (r >> 18)) | ((0x80 | ((r >> 12) & 0x3F)) << 8) | ((0x80 | ((r >> 6) & 0x3F)) << 16) |
+         ((0x80 | (r & 0x3F)) << 24);
+    return 4;
+}
 AJX_HD uint32_t utf8_put(uint32_t r, uint8_t* o) {
     if (r > 0x10FFFF || (r >= 0xD800 && r <= 0xDFFF)) r = 0xFFFD;
     if (r < 0x80) { o[0] = (uint8_t)r; return 1; }
@@ -185,7 +198,16 @@ struct NumCanon {
     uint8_t neg;
     uint8_t nd;     // significant digits (<= 17)
     int16_t dp;     // value = 0.D * 10^dp
-    uint8_t dig[18];
+    // the digits D, one nibble each (digit i at bits 4i of dlo, the 17th in dhi): registers,
+    // where a byte array indexed by position would live in scratch memory
+    uint64_t dlo;
+    uint8_t dhi;
+    AJX_HD void set_dig(int i, uint8_t c) {
+        const uint64_t v = (uint64_t)(c - '0') & 0xFull;
+        if (i < 16) dlo = (dlo & ~(0xFull << (4 * i))) | (v << (4 * i));
+        else dhi = (uint8_t)v;
+    }
+    AJX_HD int dig_at(int i) const { return '0' + (int)(i < 16 ? (dlo >> (4 * i)) & 0xFull : dhi); }
 };
 
 AJX_HD uint8_t lower_c(uint8_t c) { return c | 0x20; }
@@ -194,6 +216,8 @@ AJX_HD void num_canon(const uint8_t* s, uint32_t n, NumCanon* o) {
     o->neg = 0;
     o->nd = 0;
     o->dp = 0;
+    o->dlo = 0;
+    o->dhi = 0;
     // strconv.special: [+-]inf / [+-]infinity / nan (case-insensitive), whole string
     {
         uint32_t i = 0;
@@ -235,7 +259,7 @@ AJX_HD void num_canon(const uint8_t* s, uint32_t n, NumCanon* o) {
             continue;
         }
         seen = true;
-        if (nsig < 16) o->dig[nsig] = c;
+        if (nsig < 16) o->set_dig(nsig, c);
         nsig++;
         if (c != '0') last_nz = nsig;
         if (!sawdot) dp++;
@@ -330,7 +354,11 @@ AJX_COLD void num_canon_exact(const uint8_t* s, uint32_t n, NumCanon* o) {
     if (fb == 0) { o->kind = NumCanon::K_ZERO; return; }  // underflow: +-0
     if (fb >= 0x7FF0000000000000ull) { o->kind = neg ? NumCanon::K_NINF : NumCanon::K_PINF; return; }
     int ond, odp;
-    f64_shortest(f, o->dig, &ond, &odp, N, t, u);
+    uint8_t dg[18];  // (the exact path only)
+    f64_shortest(f, dg, &ond, &odp, N, t, u);
+    o->dlo = 0;
+    o->dhi = 0;
+    for (int i = 0; i < ond; i++) o->set_dig(i, dg[i]);
     o->kind = NumCanon::K_DIGITS;
     o->nd = (uint8_t)ond;
     o->dp = (int16_t)odp;
@@ -344,7 +372,7 @@ struct StrSrc {
     uint8_t kind;
     uint8_t bn, bi;
     bool done;
-    uint8_t buf[4];
+    uint32_t bufw;  // an escape's UTF-8 bytes, low byte first
     NumCanon num;
     int32_t pos;  // S_NUM output position
     int32_t total;
@@ -391,18 +419,18 @@ struct StrSrc {
         int intlen = dp > 0 ? dp : 1;
         if (k < intlen) {
             if (dp <= 0) return '0';
-            return k < nd ? num.dig[k] : '0';
+            return k < nd ? num.dig_at(k) : '0';
         }
         if (k == intlen) return '.';
         int j = dp + (k - intlen - 1);  // digit index in 0.D*10^dp coordinates
         if (j < 0 || j >= nd) return '0';
-        return num.dig[j];
+        return num.dig_at(j);
     }
     AJX_HD int next() {
         if (kind == S_RAW) return i < n ? p[i++] : -1;
         if (kind == S_NUM) return pos < total ? num_char(pos++) : -1;
         // S_UNESC (gjson unescape)
-        if (bi < bn) return buf[bi++];
+        if (bi < bn) return (int)((bufw >> (8u * bi++)) & 0xFFu);
         if (done || i >= n) return -1;
         uint8_t c = p[i];
         if (c < ' ') { done = true; return -1; }
@@ -434,9 +462,9 @@ struct StrSrc {
                         i += 6;
                     }
                 }
-                bn = (uint8_t)utf8_put(r, buf);
+                bn = (uint8_t)utf8_put32(r, &bufw);
                 bi = 1;
-                return buf[0];
+                return (int)(bufw & 0xFFu);
             }
             default: done = true; return -1;
         }
@@ -456,11 +484,11 @@ AJX_HD bool string_of(const uint8_t* d, const ValueRef& v, StrSrc* s) {
         case T_NUMBER: {
             if (v.esc == kValCount) {  // an element count: its decimal digits
                 uint32_t x = v.start, nd = 0;
-                uint8_t rev[10];
-                do { rev[nd++] = (uint8_t)('0' + x % 10u); x /= 10u; } while (x);
+                for (uint32_t y = x; ; y /= 10u) { nd++; if (y < 10u) break; }
                 s->kind = StrSrc::S_NUM; s->bn = s->bi = 0; s->done = false; s->pos = 0;
                 s->num.kind = NumCanon::K_DIGITS; s->num.neg = 0; s->num.nd = (uint8_t)nd; s->num.dp = (int16_t)nd;
-                for (uint32_t j = 0; j < nd; j++) s->num.dig[j] = rev[nd - 1 - j];
+                s->num.dlo = 0; s->num.dhi = 0;
+                for (int j = (int)nd - 1; j >= 0; j--, x /= 10u) s->num.set_dig(j, (uint8_t)('0' + x % 10u));
                 s->total = (int32_t)nd;
                 return true;
             }
@@ -758,21 +786,23 @@ struct ArrIter {
 // ---------------------------------------------------------------------------------
 struct RuneReader {
     StrSrc* src;
-    uint8_t la[4];
+    uint32_t law;  // the look-ahead bytes, low byte first (registers, not a byte array)
     int nla;
-    AJX_HD void init(StrSrc* s) { src = s; nla = 0; }
+    AJX_HD void init(StrSrc* s) { src = s; nla = 0; law = 0; }
+    AJX_HD uint32_t la(int k) const { return (law >> (8 * k)) & 0xFFu; }
     AJX_HD void fill() {
         while (nla < 4) {
             int c = src->next();
             if (c < 0) break;
-            la[nla++] = (uint8_t)c;
+            law |= (uint32_t)(c & 0xFF) << (8 * nla);
+            nla++;
         }
     }
     // Go utf8.DecodeRune; returns -1 at end
     AJX_HD int32_t next() {
         fill();
         if (nla == 0) return -1;
-        uint32_t b0 = la[0];
+        uint32_t b0 = la(0);
         int sz = 1;
         uint32_t r = 0xFFFD;
         if (b0 < 0x80) {
@@ -790,17 +820,17 @@ struct RuneReader {
                 if (b0 == 0xF0) lo = 0x90;
                 if (b0 == 0xF4) hi = 0x8F;
             }
-            if (need && nla >= need && la[1] >= lo && la[1] <= hi) {
+            if (need && nla >= need && la(1) >= lo && la(1) <= hi) {
                 bool good = true;
-                v = (v << 6) | (la[1] & 0x3F);
+                v = (v << 6) | (la(1) & 0x3F);
                 for (int k = 2; k < need; k++) {
-                    if (la[k] < 0x80 || la[k] > 0xBF) { good = false; break; }
-                    v = (v << 6) | (la[k] & 0x3F);
+                    if (la(k) < 0x80 || la(k) > 0xBF) { good = false; break; }
+                    v = (v << 6) | (la(k) & 0x3F);
                 }
                 if (good) { r = v; sz = need; }
             }
         }
-        for (int k = sz; k < nla; k++) la[k - sz] = la[k];
+        law = sz >= 4 ? 0u : law >> (8 * sz);
         nla -= sz;
         return (int32_t)r;
     }
