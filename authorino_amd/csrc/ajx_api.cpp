@@ -22,6 +22,7 @@ struct authjx_ruleset {
     uint8_t* d_blob = nullptr;
     ajx::CompiledRuleset c;
     bool stream_ok = false;  // the streaming kernel takes it (ajx::stream_eligible)
+    uint32_t stream_rec = 0;  // its capture records there (ajx::stream_records)
     // workspaces (by registry id) whose stream has run a batch over this ruleset:
     // authjx_free waits for their last batch instead of the whole device
     std::mutex mu;
@@ -438,6 +439,7 @@ int finish_compile(authjx_ctx* ctx, authjx_ruleset* rs, int rc, const std::strin
         for (uint32_t i = 0; i < rs->c.n_patterns; i++) pattern_status[i] = rs->c.pattern_status[i];
     rs->device = ctx->device;
     rs->stream_ok = ajx::stream_eligible(rs->c.blob.data(), (uint32_t)rs->c.blob.size());
+    rs->stream_rec = ajx::stream_records(rs->c.blob.data());
     if (hipSetDevice(ctx->device) != hipSuccess ||
         hipMalloc(&rs->d_blob, rs->c.blob.size()) != hipSuccess ||
         hipMemcpy(rs->d_blob, rs->c.blob.data(), rs->c.blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -529,7 +531,9 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         per = 1;
     else if (ablate == 0)
         per = std::max<uint32_t>(1u, std::min<uint32_t>(ajx::kStreamSpan, (n + 2047u) / 2048u));
-    const uint32_t rows_stride = use_stream ? row_stride + 4u : row_stride;
+    uint32_t max_rec = 0;
+    for (uint32_t i = 0; i < n_sets; i++) max_rec = std::max(max_rec, sets[i]->stream_rec);
+    const uint32_t rows_stride = use_stream ? std::max(row_stride, 1u + max_rec) + 4u : row_stride;
     if (!force_scan) {
         rc = ensure_work(w, n, rows_stride);
         if (rc != AUTHJX_OK) return rc;
@@ -561,7 +565,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         // the streaming kernel (ajx_stream.h; ablate 50: its structural pass alone, 51: no
         // fold), its stage B over the d_perm buffer as the stage-B list
         w->rows_stride = rows_stride;
-        HIP_OK(ajx::launch_eval_stream(w->d_sets, d_set_of_req, (uint32_t)sets[0]->c.blob.size(), max_sel, d_arena,
+        HIP_OK(ajx::launch_eval_stream(w->d_sets, d_set_of_req, (uint32_t)sets[0]->c.blob.size(), max_rec, d_arena,
                                        d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap,
                                        bitmap_stride_words, w->d_rows, rows_stride, keep_rows, w->d_perm, w->d_slow,
                                        w->d_slow + 2, s, ablate == 50 ? 1 : ablate == 51 ? 2 : 0, mods, per));

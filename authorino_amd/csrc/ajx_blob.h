@@ -266,11 +266,19 @@ struct StreamHdr {
     uint32_t off_paths, path_log2, path_mult, path_probes;  // StreamPathSlot[1 << path_log2]
     uint32_t n_keys, max_key_len;
     uint32_t light;  // every pattern is an eager one (EagerSel): stage B is the fold alone
-    uint32_t pad;
-    // selectors the stream does not follow (an array index, more than kStreamMaxComps
-    // components, a key longer than kStreamMaxKeyLen): stage B takes their values with the
-    // exact Get on the proved document
-    uint32_t exact_lo, exact_hi, pad2[2];
+    uint32_t n_rec;  // capture records per request: the selectors', then the extra prefixes'
+    // selectors the stream does not follow to the end (an array index, more than
+    // kStreamMaxComps components, a key longer than kStreamMaxKeyLen): stage B takes their
+    // values with the exact Get inside their longest followed prefix's captured value
+    // (StreamTail), or on the whole proved document
+    uint32_t exact_lo, exact_hi;
+    uint32_t off_tails, n_tails;  // StreamTail[n_tails]
+};
+struct StreamTail {
+    uint16_t sel;         // the selector
+    uint16_t slot;        // the record of its prefix's value (0xFFFF: no prefix, whole document)
+    uint16_t comp_begin;  // the rest of its path: components [comp_begin, comp_begin + comp_count)
+    uint16_t comp_count;
 };
 
 AJX_BLOB_HD inline uint32_t stream_path_hash(uint64_t p, uint32_t log2, uint32_t mult) {

@@ -844,17 +844,52 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 return trie[w.node].keys[j].second < 0 && trie[w.node].keys[j].first.size() <= kStreamMaxKeyLen &&
                        w.depth < kStreamMaxComps;
             };
+            // an exact selector's longest prefix the stream follows: its record is the
+            // prefix node's selector's, or an extra one after the selectors' (the stream
+            // captures that value, stage B runs the rest of the path inside it)
+            std::map<uint32_t, uint32_t> extra;  // trie node -> record
+            std::vector<StreamTail> tails;
+            uint32_t nrec = (uint32_t)sels.size();
+            for (size_t si = 0; si < sels.size(); si++) {
+                if (!((sexact >> si) & 1ull)) continue;
+                uint32_t node = 0, k = 0;
+                for (; k < sels[si].comp_count && k < kStreamMaxComps; k++) {
+                    const Component& c = comps[sels[si].comp_begin + k];
+                    if (c.array_index >= 0 || c.lit_len > kStreamMaxKeyLen) break;
+                    const std::string key = lits.substr(c.lit_off, c.lit_len);
+                    uint32_t next = 0;
+                    for (size_t j = 0; j < trie[node].kids.size() && !next; j++)
+                        if (trie[node].keys[j].second < 0 && trie[node].keys[j].first == key) next = trie[node].kids[j];
+                    if (!next) break;
+                    node = next;
+                }
+                uint32_t slot = 0xFFFFu;
+                if (k > 0) {
+                    if (trie[node].selector >= 0) {
+                        slot = (uint32_t)trie[node].selector;
+                    } else {
+                        auto it = extra.find(node);
+                        if (it == extra.end()) it = extra.emplace(node, nrec++).first;
+                        slot = it->second;
+                    }
+                }
+                tails.push_back(StreamTail{(uint16_t)si, (uint16_t)slot, (uint16_t)(sels[si].comp_begin + k),
+                                           (uint16_t)(sels[si].comp_count - k)});
+            }
+            if (nrec > kFastMaxSelectors) stream_ok = false;  // (found bits)
             std::vector<Walk> stack{{0u, 0ull, 0u}};
             while (!stack.empty() && stream_ok) {
                 const Walk w = stack.back();
                 stack.pop_back();
-                // (a node's meta: its selector, 0xFFFF none; kStreamHasKids when keys the stream
-                // follows go on below it)
+                // (a node's meta: its record — its selector, an exact selector's prefix — 0xFFFF
+                // none; kStreamHasKids when keys the stream follows go on below it)
                 bool kids = false;
                 for (size_t j = 0; j < trie[w.node].kids.size(); j++) kids = kids || stream_edge(j, w);
-                if (w.node && (trie[w.node].selector >= 0 || kids))
-                    paths.push_back({w.path, (trie[w.node].selector >= 0 ? (uint32_t)trie[w.node].selector : 0xFFFFu) |
-                                                 (kids ? kStreamHasKids : 0u)});
+                const auto xt = extra.find(w.node);
+                const uint32_t rec = trie[w.node].selector >= 0 ? (uint32_t)trie[w.node].selector
+                                     : xt != extra.end()       ? xt->second
+                                                               : 0xFFFFu;
+                if (w.node && (rec != 0xFFFFu || kids)) paths.push_back({w.path, rec | (kids ? kStreamHasKids : 0u)});
                 for (size_t j = 0; j < trie[w.node].kids.size(); j++) {
                     const std::string& key = trie[w.node].keys[j].first;
                     if (!stream_edge(j, w)) continue;  // (the selectors below: exact Get)
@@ -944,6 +979,8 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 sh.light = light && !sexact ? 1u : 0u;
                 sh.exact_lo = (uint32_t)sexact;
                 sh.exact_hi = (uint32_t)(sexact >> 32);
+                sh.n_rec = nrec;
+                sh.n_tails = (uint32_t)tails.size();
                 hdr.off_stream = (uint32_t)b.align16();
                 b.append(&sh, sizeof sh);
                 StreamHdr* shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
@@ -952,6 +989,9 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
                 shp->off_paths = (uint32_t)b.align16();
                 b.append(pslots.data(), pslots.size() * sizeof(StreamPathSlot));
+                shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
+                shp->off_tails = (uint32_t)b.align16();
+                b.append(tails.data(), tails.size() * sizeof(StreamTail));
             }
         }
         std::vector<SelectorPatterns> sp(sels.size());

@@ -54,17 +54,19 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
 
 // The streaming kernel (ajx_stream.h), its stage B (ajx_stream_finish) and the exact scan of
 // what they hand over: one ruleset for the batch (sets[0], staged in LDS); stream_eligible
-// says whether it can take the ruleset. d_rows: rows of row_stride >= 5 + n_selectors
+// says whether it can take the ruleset. d_rows: rows of row_stride >= 5 + n_rec
 // words for n requests (wave layout, work-item = request): the rows stage B reads, and with
 // keep_rows every request's row for authjx_select_from_eval_device. d_stage_ids: n u32;
 // d_slow_count[1] (the stage-B count) follows the slow count. mode (profiling): 1 the structural pass alone, 2 no fold. per: requests per wave
 // (1..32, 0 = 32): fewer for small batches, so more waves share the walk. d_set_of_req
 // (a multi-tenant batch, every ruleset stream-eligible): one request per wave under its
-// own ruleset, tables from global memory; n_selectors then the largest of the batch.
+// own ruleset, tables from global memory; n_rec then the largest of the batch.
 bool stream_eligible(const uint8_t* host_blob, uint32_t blob_bytes);
+// capture records of the streaming kernel's rows (n_selectors + exact selectors' prefixes)
+uint32_t stream_records(const uint8_t* host_blob);
 constexpr uint32_t kStreamSpan = 32;  // requests per wave at most (stream::kSpan)
 hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t blob_bytes,
-                              uint32_t n_selectors, const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                              uint32_t n_rec, const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                               uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                               uint32_t row_stride, bool keep_rows, uint32_t* d_stage_ids, uint32_t* d_slow_count,
                               uint32_t* d_slow_ids, hipStream_t stream, int mode = 0, bool mods = false,

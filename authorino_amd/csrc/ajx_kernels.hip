@@ -517,7 +517,7 @@ constexpr uint32_t kStageExact = 1u << 31;
 // arena order and reads their bytes as one coalesced stream; a lane per request then folds
 // the patterns the stream decided. Requests with a pattern left (a value to parse or
 // unescape, a regex, a long value) go with their row (found word, records, the 4 eager
-// words: row_stride >= 5 + n_selectors) to ajx_stream_finish through the stage-B list;
+// words: row_stride >= 5 + n_rec, StreamHdr) to ajx_stream_finish through the stage-B list;
 // requests it can not prove go to the slow list (the exact scan). keep_rows (forest
 // rulesets, for authjx_select_from_eval_device): every request's row is written (slow
 // ones: kRowSlow), those with an open record through stage B. Rows: the wave-interleaved
@@ -583,7 +583,9 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
         if (keep_rows) o[0] = kRowSlow;
         return;
     }
-    const uint32_t ns = reinterpret_cast<const RulesetHdr*>(blob)->n_selectors;
+    // (the records: the selectors', then exact selectors' prefixes')
+    const RulesetHdr* hb = reinterpret_cast<const RulesetHdr*>(blob);
+    const uint32_t ns = reinterpret_cast<const StreamHdr*>(blob + hb->off_stream)->n_rec;
     bool open = false;
     if (keep_rows)
         for (uint32_t s = 0; s < ns; s++) open = open || ((rowp[1u + s] >> 32) & stream::kOpenEnd);
@@ -645,18 +647,23 @@ bool stream_eligible(const uint8_t* host_blob, uint32_t blob_bytes) {
            h->n_selectors <= kFastMaxSelectors;
 }
 
+uint32_t stream_records(const uint8_t* host_blob) {
+    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(host_blob);
+    return h->off_stream ? reinterpret_cast<const StreamHdr*>(host_blob + h->off_stream)->n_rec : h->n_selectors;
+}
+
 static_assert(kStreamSpan == stream::kSpan, "requests per wave");
 
 // 4-wave workgroups (the kernel's launch bounds), each with its own blob copy
 constexpr uint32_t kStreamBlock = 256;
 
 hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t blob_bytes,
-                              uint32_t n_selectors, const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
+                              uint32_t n_rec, const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                               uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                               uint32_t row_stride, bool keep_rows, uint32_t* d_stage_ids, uint32_t* d_slow_count,
                               uint32_t* d_slow_ids, hipStream_t stream, int mode, bool mods, uint32_t per) {
     if (n == 0) return hipSuccess;
-    if (row_stride < 5u + n_selectors) return hipErrorInvalidValue;
+    if (row_stride < 5u + n_rec) return hipErrorInvalidValue;
     const bool mt = d_set_of_req != nullptr;
     if (mt) {
         if (mode != 0) return hipErrorInvalidValue;
@@ -664,7 +671,7 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
         blob_bytes = 0;  // (no blob copy: each wave reads its ruleset from global memory)
     }
     const uint32_t wave_off = (blob_bytes + 15u) & ~15u;
-    const uint32_t wave_bytes = (stream::lds_bytes(n_selectors) + 15u) & ~15u;
+    const uint32_t wave_bytes = (stream::lds_bytes(n_rec) + 15u) & ~15u;
     const uint32_t block = kStreamBlock;
     const uint32_t lds = wave_off + (block / 64) * wave_bytes;
     if (lds > 160u * 1024u) return hipErrorInvalidValue;

@@ -185,6 +185,7 @@ struct Tabs {
     const EagerSel* eg;  // (null: none)
     const uint8_t* lits;
     uint32_t k_log2, k_mult, k_probes, p_log2, p_mult, p_probes, max_key_len, ns;
+    uint32_t nr;     // capture records (the selectors', then exact selectors' prefixes')
     uint32_t exact;  // some selector takes the exact Get in stage B (StreamHdr exact_lo / hi)
 };
 AJX_HD Tabs tabs_of(const uint8_t* blob) {
@@ -203,6 +204,7 @@ AJX_HD Tabs tabs_of(const uint8_t* blob) {
     t.p_probes = lean::uni(s->path_probes);
     t.max_key_len = lean::uni(s->max_key_len);
     t.ns = lean::uni(h->n_selectors);
+    t.nr = lean::uni(s->n_rec);
     t.exact = lean::uni(s->exact_lo | s->exact_hi);
     return t;
 }
@@ -675,9 +677,8 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
         const uint32_t OPE = T.eg ? OP & ~nCO : 0u;
         const uint32_t want = keym | ELQ | ELS | OPE;
         if (want) {
-            const uint32_t ns = T.ns;
-            uint64_t* row = rows + (size_t)doc * (1u + ns);
-            uint64_t* dec = rows + (size_t)kSpan * (1u + ns) + 4u * doc;
+            uint64_t* row = rows + (size_t)doc * (1u + T.nr);
+            uint64_t* dec = rows + (size_t)kSpan * (1u + T.nr) + 4u * doc;
             int32_t dd = depth_in;
             uint64_t iv = (uint64_t)stk_in.iv0 | ((uint64_t)stk_in.iv1 << 32);
             // the selector whose path is the container at level dd (kNone: none)
@@ -688,7 +689,8 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                 const uint64_t pth = iv & keep;
                 if (((pth - 0x0101010101010101ull) & ~pth & 0x8080808080808080ull) & keep) return kNone;
                 const uint32_t pm = path_meta(T, pth);
-                return (pm && (pm & 0xFFFFu) != 0xFFFFu) ? (pm & 0xFFFFu) : kNone;
+                // (a selector's: its eager tables; an exact selector's prefix record has none)
+                return (pm && (pm & 0xFFFFu) < T.ns) ? (pm & 0xFFFFu) : kNone;
             };
             for (uint32_t m = (OP | CL | want) & below(hib(want) + 1u); m; m &= m - 1u) {
                 const uint32_t i = ctz(m);
@@ -840,7 +842,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                                            : (((end - vpos) & 0xFFFFFFu) | (type << 24) | (esc << 27));
                 reinterpret_cast<uint32_t*>(&row[1u + s])[1] = meta;
                 // eager patterns on the value's text
-                if (T.eg && tn != 0xFFFFFFFFu) {
+                if (T.eg && tn != 0xFFFFFFFFu && s < T.ns) {
                     const EagerSel eg = T.eg[s];
                     const uint32_t hit = eager_hits(eg, ring, ta, tn);
                     uint64_t dD = 0, dT = 0;
@@ -1004,40 +1006,56 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
                         uint32_t stride, const uint64_t* dwp = nullptr) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const uint32_t ns = h->n_selectors;
+    const StreamHdr* sh = reinterpret_cast<const StreamHdr*>(blob + h->off_stream);
+    const uint32_t nr = sh->n_rec;
     const EagerSel* eg = h->off_eager ? reinterpret_cast<const EagerSel*>(blob + h->off_eager) : nullptr;
-    const uint64_t dw[4] = {dwp ? dwp[0] : row[1u + ns], dwp ? dwp[1] : row[2u + ns], dwp ? dwp[2] : row[3u + ns],
-                            dwp ? dwp[3] : row[4u + ns]};
+    const uint64_t dw[4] = {dwp ? dwp[0] : row[1u + nr], dwp ? dwp[1] : row[2u + nr], dwp ? dwp[2] : row[3u + nr],
+                            dwp ? dwp[3] : row[4u + nr]};
     uint64_t dD = dw[0], dT = dw[1];
     array_decisions(eg, ns, row, dw, dD, dT);
-    // the selectors the stream does not follow: the exact Get on the proved document
-    const StreamHdr* sh = reinterpret_cast<const StreamHdr*>(blob + h->off_stream);
-    const uint64_t exact = (uint64_t)sh->exact_lo | ((uint64_t)sh->exact_hi << 32);
-    if (exact) {
-        const Selector* sels = reinterpret_cast<const Selector*>(blob + h->off_selectors);
-        const Component* comps = reinterpret_cast<const Component*>(blob + h->off_components);
-        const uint8_t* lits = blob + h->off_literals;
-        for (uint64_t m = exact; m; m &= m - 1ull) {
-            const uint32_t s = (uint32_t)__builtin_ctzll(m);
-            const ValueRef v = gj_get(d, n, comps + sels[s].comp_begin, sels[s].comp_count, lits);
-            if (v.type == T_NULL && v.start == v.end) continue;  // (not found: Null)
-            row[1u + s] = (uint64_t)v.start |
-                          ((uint64_t)(((v.end - v.start) & 0xFFFFFFu) | ((uint32_t)v.type << 24) |
-                                      ((uint32_t)(v.esc & 1u) << 27)) << 32);
-            row[0] = row[0] | (1ull << s);
-        }
-    }
     const SelectorPatterns* sps = reinterpret_cast<const SelectorPatterns*>(blob + h->off_sel_patterns);
-    for (uint32_t s = 0; s < ns; s++) {
+    for (uint32_t s = 0; s < nr; s++) {
         uint64_t rec = row[1u + s];
         if ((uint32_t)rec == kNone || !((rec >> 32) & kOpenEnd)) continue;
         // (every pattern of the selector decided already: its value is not read; a forest's
         // rows are kept for authjx_select_from_eval_device, whose values must all be closed)
-        if (!h->pad1[0] && !(sps[s].mask[0] & ~dD) && !sps[s].mask[1]) continue;
+        if (s < ns && !h->pad1[0] && !(sps[s].mask[0] & ~dD) && !sps[s].mask[1]) continue;
         if (!resolve_open(d, n, (uint32_t)rec, &rec)) {
             row[0] = kRowSlow;
             return false;
         }
         row[1u + s] = rec;
+    }
+    // the selectors the stream does not follow to the end: the exact Get of the rest of the
+    // path inside their prefix's value (or on the whole proved document)
+    if (sh->n_tails) {
+        const Selector* sels = reinterpret_cast<const Selector*>(blob + h->off_selectors);
+        const Component* comps = reinterpret_cast<const Component*>(blob + h->off_components);
+        const StreamTail* tl = reinterpret_cast<const StreamTail*>(blob + sh->off_tails);
+        const uint8_t* lits = blob + h->off_literals;
+        for (uint32_t k = 0; k < sh->n_tails; k++) {
+            const StreamTail e = tl[k];
+            ValueRef v;
+            v.type = T_NULL;
+            v.start = v.end = 0;
+            bool whole = e.slot == 0xFFFFu;
+            if (!whole) {
+                const uint64_t pre = row[1u + e.slot];
+                if ((uint32_t)pre == kNone) continue;  // (no prefix: not found)
+                const uint32_t a = (uint32_t)pre, len = (uint32_t)(pre >> 32) & 0xFFFFFFu;
+                v = gj_get(d + a, len, comps + e.comp_begin, e.comp_count, lits);
+                v.start += a;
+                v.end += a;
+                // (not inside the first match of the prefix: the whole document decides)
+                whole = v.type == T_NULL && v.start == v.end;
+            }
+            if (whole) v = gj_get(d, n, comps + sels[e.sel].comp_begin, sels[e.sel].comp_count, lits);
+            if (v.type == T_NULL && v.start == v.end) continue;  // (not found: Null)
+            row[1u + e.sel] = (uint64_t)v.start |
+                              ((uint64_t)(((v.end - v.start) & 0xFFFFFFu) | ((uint32_t)v.type << 24) |
+                                          ((uint32_t)(v.esc & 1u) << 27)) << 32);
+            row[0] = row[0] | (1ull << e.sel);
+        }
     }
     uint64_t t[2], u[2];
     const uint64_t dec[2] = {dD, dT};
@@ -1088,7 +1106,7 @@ AJX_HD uint32_t scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const
     const uint64_t off = my ? offs[r] : 0ull;
     const uint32_t len = my ? lens[r] : 0u;
     uint32_t my_start, total;
-    span_setup(L, rows, T.ns, l, my, off, len, my_start, total);
+    span_setup(L, rows, T.nr, l, my, off, len, my_start, total);
     Carry c;
     carry_init(c);
     const uint32_t nsteps = (total + 63u) / 64u;
@@ -1120,8 +1138,8 @@ AJX_HD uint32_t scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const
         const DocEnt e = L.doc[l];
         *lds_doc = L.ring_raw + 16 + 64 + e.start * 32u + (e.len_mis >> 24);
     }
-    uint64_t* row = rows + (size_t)l * (1u + T.ns);
-    const uint64_t* dp = rows + (size_t)kSpan * (1u + T.ns) + 4u * l;
+    uint64_t* row = rows + (size_t)l * (1u + T.nr);
+    const uint64_t* dp = rows + (size_t)kSpan * (1u + T.nr) + 4u * l;
     *row_out = row;
     *dw_out = dp;
     uint64_t found = 0;

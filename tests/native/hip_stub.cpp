@@ -122,6 +122,7 @@ hipError_t launch_eval_fast(const uint8_t* const*, const uint32_t*, uint32_t, co
     return hipSuccess;
 }
 bool stream_eligible(const uint8_t*, uint32_t) { return true; }
+uint32_t stream_records(const uint8_t*) { return 1; }
 hipError_t launch_eval_stream(const uint8_t* const*, const uint32_t*, uint32_t, uint32_t, const uint8_t*,
                               const uint64_t*, const uint32_t*, uint32_t n, uint8_t* tri, int32_t* err, uint64_t* bm,
                               uint32_t stride, uint64_t* rows, uint32_t row_stride, bool keep_rows,

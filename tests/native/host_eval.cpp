@@ -334,7 +334,7 @@ extern "C" int ht_eval_stream(void* h, const uint8_t* arena, const uint64_t* off
     std::vector<uint64_t> blob_buf((blob_v.size() + 7) / 8 + 2);
     std::memcpy(blob_buf.data(), blob_v.data(), blob_v.size());
     const uint8_t* blob = (const uint8_t*)blob_buf.data();
-    const uint32_t ns = hd->n_selectors;
+    const uint32_t ns = reinterpret_cast<const StreamHdr*>(blob_v.data() + hd->off_stream)->n_rec;  // (records)
     if (per == 0 || per > stream::kSpan) per = stream::kSpan;
     const uint32_t spans = (n + per - 1) / per;
     std::vector<uint64_t> wl(stream::lds_bytes(ns) / 8 + 2);
