@@ -565,7 +565,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         // the streaming kernel (ajx_stream.h; ablate 50: its structural pass alone, 51: no
         // fold), its stage B over the d_perm buffer as the stage-B list
         w->rows_stride = rows_stride;
-        HIP_OK(ajx::launch_eval_stream(w->d_sets, d_set_of_req, (uint32_t)sets[0]->c.blob.size(), max_rec, d_arena,
+        HIP_OK(ajx::launch_eval_stream(w->d_sets, d_set_of_req, (uint32_t)max_blob, max_rec, d_arena,
                                        d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap,
                                        bitmap_stride_words, w->d_rows, rows_stride, keep_rows, w->d_perm, w->d_slow,
                                        w->d_slow + 2, s, ablate == 50 ? 1 : ablate == 51 ? 2 : 0, mods, per));

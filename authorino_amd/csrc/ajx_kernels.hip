@@ -545,13 +545,26 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
     const uint32_t span = blockIdx.x * (blockDim.x >> 6) + w;
     const uint8_t* blob;
+    uint8_t* base;
     if constexpr (MT) {
+        // per wave: [its ruleset's blob, when it fits wave_off bytes] [WaveLds, rows]
         if (span >= n) return;  // (wave-uniform; per = 1)
-        blob = sets[set_of_req[span]];
+        const uint8_t* g = sets[set_of_req[span]];
+        uint8_t* wb = reinterpret_cast<uint8_t*>(s_stream_dyn) + w * wave_bytes;
+        const uint32_t tb = lean::uni(reinterpret_cast<const RulesetHdr*>(g)->total_bytes);  // (x16)
+        if (tb <= wave_off) {
+            for (uint32_t i = l; i < tb / 16u; i += 64u)
+                reinterpret_cast<uint4*>(wb)[i] = reinterpret_cast<const uint4*>(g)[i];
+            wave::sync();
+            blob = wb;
+        } else {
+            blob = g;
+        }
+        base = wb + wave_off;
     } else {
         blob = stage_blob<true>(sets[0]);
+        base = reinterpret_cast<uint8_t*>(s_stream_dyn) + wave_off + w * wave_bytes;
     }
-    uint8_t* base = reinterpret_cast<uint8_t*>(s_stream_dyn) + wave_off + w * wave_bytes;
     stream::WaveLds& L = *reinterpret_cast<stream::WaveLds*>(base);
     uint64_t* rows = reinterpret_cast<uint64_t*>(base + sizeof(stream::WaveLds));
     if (span * per >= n) return;  // (wave-uniform)
@@ -668,12 +681,21 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
     if (mt) {
         if (mode != 0) return hipErrorInvalidValue;
         per = 1;
-        blob_bytes = 0;  // (no blob copy: each wave reads its ruleset from global memory)
     }
-    const uint32_t wave_off = (blob_bytes + 15u) & ~15u;
-    const uint32_t wave_bytes = (stream::lds_bytes(n_rec) + 15u) & ~15u;
+    uint32_t wave_off = (blob_bytes + 15u) & ~15u;
+    uint32_t wave_bytes = (stream::lds_bytes(n_rec) + 15u) & ~15u;
+    if (mt) {
+        // each wave copies its own ruleset's blob next to its LDS when it fits (blob_bytes:
+        // the batch's largest), else reads it from global memory: wave_off is that room
+        const uint32_t room = 160u * 1024u / (kStreamBlock / 64u);
+        uint32_t cap = wave_off;
+        if (cap + wave_bytes > room) cap = room > wave_bytes ? (room - wave_bytes) & ~15u : 0u;
+        if (cap < 1024u) cap = 0;
+        wave_off = cap;
+        wave_bytes += cap;
+    }
     const uint32_t block = kStreamBlock;
-    const uint32_t lds = wave_off + (block / 64) * wave_bytes;
+    const uint32_t lds = (mt ? 0u : wave_off) + (block / 64) * wave_bytes;
     if (lds > 160u * 1024u) return hipErrorInvalidValue;
     if (per == 0 || per > stream::kSpan) per = stream::kSpan;
     // a small batch (fewer requests per wave, or one per wave under its own ruleset): stage B
