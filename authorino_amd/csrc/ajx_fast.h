@@ -1101,8 +1101,10 @@ AJX_HD bool incl_hits(const uint8_t* doc, const ValueRef& v, const Pattern* pats
 
 // Stage B for one request: patterns on the captured values, bitmap, fold.
 // res(p) values are V_T / V_F / V_E / V_U.
+// (s0, sstep: the selectors s0, s0 + sstep, ... only — the lanes of a wave sharing one
+// request's stage B; their t / u OR together)
 AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef row, uint64_t t[2],
-                              uint64_t u[2], const uint64_t* dec = nullptr) {
+                              uint64_t u[2], const uint64_t* dec = nullptr, uint32_t s0 = 0, uint32_t sstep = 1) {
     // selector by selector: each captured value is decoded once for all its patterns;
     // when its String() is a byte span or a literal, eq/neq compare a dword at a time,
     // `matches` runs the DFA straight over the span and incl/excl walk a compact array
@@ -1116,7 +1118,7 @@ AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef ro
     uint64_t t0 = 0, t1 = 0, u0 = h->unsupported[0], u1 = h->unsupported[1];
     const uint64_t nt0 = h->null_true[0], nt1 = h->null_true[1];
     const uint32_t ns = h->n_selectors;
-    for (uint32_t s = 0; s < ns; s++) {
+    for (uint32_t s = s0; s < ns; s += sstep) {
         const uint32_t cnt = sps[s].count;
         if (!cnt) continue;
         if (!((found >> s) & 1)) {  // Null result

@@ -573,6 +573,27 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
     const uint32_t res = stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
                                                  out_bm, stride, &rowp, &dwp, LAT ? &lds_doc : nullptr);
     const uint32_t r = span * per + l;
+    if constexpr (LAT) {
+        // one request per wave: every lane takes part in its stage B (finish_full<true>)
+        if (per == 1 && wave::readlane(res == stream::R_STAGE_B && lds_doc ? 1u : 0u, 0) != 0) {
+            auto bcast = [](const void* q) {  // lane 0's pointer
+                const uint64_t v = (uint64_t)(uintptr_t)q;
+                return (uintptr_t)((uint64_t)wave::readlane((uint32_t)v, 0) |
+                                   ((uint64_t)wave::readlane((uint32_t)(v >> 32), 0) << 32));
+            };
+            const uint8_t* d0 = reinterpret_cast<const uint8_t*>(bcast(lds_doc));
+            const uint64_t* row0 = reinterpret_cast<const uint64_t*>(bcast(rowp));
+            const uint64_t* dw0 = reinterpret_cast<const uint64_t*>(bcast(dwp));
+            const uint32_t r0 = span;
+            const bool ok = stream::finish_full<true>(r0, blob, d0, lens[r0], RowRef(row0), out_tri, out_err, out_bm,
+                                                      stride, dw0);
+            if (!ok && l == 0) {
+                atomicAdd(slow_count, 1u);
+                stage_ids[atomicAdd(slow_count + 1, 1u)] = r0 | kStageExact;
+            }
+            return;
+        }
+    }
     if (l >= per || r >= n || MODE != 0) return;
     if constexpr (LAT) {
         if (res == stream::R_STAGE_B && lds_doc) {

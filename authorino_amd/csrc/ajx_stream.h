@@ -1001,9 +1001,19 @@ AJX_HD bool finish_light(uint32_t r, const uint8_t* blob, const Tabs& T, const u
 // the document, the arrays' decisions, ajx_fast.h's patterns_from_row, the T bitmap and the
 // fold. false: the exact scan decides the request (the row is marked kRowSlow).
 // dwp: the eager words (null: they follow the row's records, as in the stage-B rows).
+// WAVE: all 64 lanes of a wave share the one request (the row in LDS): lane l resolves the
+// records, tails and selectors l, l + 64, ...; the pattern bits meet by a wave-wide OR and
+// lane 0 writes the outputs (the result is the same on every lane).
+template <bool WAVE = false>
 AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint32_t n, RowRef row,
                         uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
                         uint32_t stride, const uint64_t* dwp = nullptr) {
+    const uint32_t lane = WAVE ? wave::lane() : 0u, step = WAVE ? 64u : 1u;
+    // (WAVE: a failure in any lane fails the request)
+    auto fail_any = [&](bool f) -> bool {
+        if constexpr (WAVE) return wave::ballot(f) != 0;
+        return f;
+    };
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const uint32_t ns = h->n_selectors;
     const StreamHdr* sh = reinterpret_cast<const StreamHdr*>(blob + h->off_stream);
@@ -1014,18 +1024,24 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
     uint64_t dD = dw[0], dT = dw[1];
     array_decisions(eg, ns, row, dw, dD, dT);
     const SelectorPatterns* sps = reinterpret_cast<const SelectorPatterns*>(blob + h->off_sel_patterns);
-    for (uint32_t s = 0; s < nr; s++) {
+    bool bad = false;
+    for (uint32_t s = lane; s < nr; s += step) {
         uint64_t rec = row[1u + s];
         if ((uint32_t)rec == kNone || !((rec >> 32) & kOpenEnd)) continue;
         // (every pattern of the selector decided already: its value is not read; a forest's
         // rows are kept for authjx_select_from_eval_device, whose values must all be closed)
         if (s < ns && !h->pad1[0] && !(sps[s].mask[0] & ~dD) && !sps[s].mask[1]) continue;
         if (!resolve_open(d, n, (uint32_t)rec, &rec)) {
-            row[0] = kRowSlow;
-            return false;
+            bad = true;
+            break;
         }
         row[1u + s] = rec;
     }
+    if (fail_any(bad)) {
+        if (lane == 0) row[0] = kRowSlow;
+        return false;
+    }
+    if constexpr (WAVE) wave::sync();
     // the selectors the stream does not follow to the end: the exact Get of the rest of the
     // path inside their prefix's value (or on the whole proved document)
     if (sh->n_tails) {
@@ -1033,7 +1049,7 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
         const Component* comps = reinterpret_cast<const Component*>(blob + h->off_components);
         const StreamTail* tl = reinterpret_cast<const StreamTail*>(blob + sh->off_tails);
         const uint8_t* lits = blob + h->off_literals;
-        for (uint32_t k = 0; k < sh->n_tails; k++) {
+        for (uint32_t k = lane; k < sh->n_tails; k += step) {
             const StreamTail e = tl[k];
             ValueRef v;
             v.type = T_NULL;
@@ -1054,16 +1070,33 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
             row[1u + e.sel] = (uint64_t)v.start |
                               ((uint64_t)(((v.end - v.start) & 0xFFFFFFu) | ((uint32_t)v.type << 24) |
                                           ((uint32_t)(v.esc & 1u) << 27)) << 32);
-            row[0] = row[0] | (1ull << e.sel);
+            if constexpr (WAVE)
+                wave::lds_or64(&row[0], 1ull << e.sel);
+            else
+                row[0] = row[0] | (1ull << e.sel);
         }
+        if constexpr (WAVE) wave::sync();
     }
     uint64_t t[2], u[2];
     const uint64_t dec[2] = {dD, dT};
-    patterns_from_row(blob, d, row, t, u, dec);
+    patterns_from_row(blob, d, row, t, u, dec, lane, step);
+    if constexpr (WAVE) {  // (OR over the lanes)
+        auto orall = [](uint64_t x) -> uint64_t {
+            const auto OR = [](uint32_t a, uint32_t b) { return a | b; };
+            const uint32_t lo = wave::readlane(wave::scan_incl((uint32_t)x, 0u, OR), 63);
+            const uint32_t hi = wave::readlane(wave::scan_incl((uint32_t)(x >> 32), 0u, OR), 63);
+            return (uint64_t)lo | ((uint64_t)hi << 32);
+        };
+        t[0] = orall(t[0]);
+        t[1] = orall(t[1]);
+        u[0] = orall(u[0]);
+        u[1] = orall(u[1]);
+    }
     if ((u[0] & ~h->unsupported[0]) | (u[1] & ~h->unsupported[1])) {
-        row[0] = kRowSlow;
+        if (lane == 0) row[0] = kRowSlow;
         return false;
     }
+    if (lane != 0) return true;
     if (out_bm) {
         uint64_t* orow = out_bm + (size_t)r * stride;
         orow[0] = t[0];

@@ -358,6 +358,21 @@ extern "C" int ht_eval_stream(void* h, const uint8_t* arena, const uint64_t* off
                 res = stream::scan_span<0>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
                                            out_bm, stride, &rowp, &dwp, lat ? &lds_doc : nullptr);
             const uint32_t r = span * per + l;
+            // (one request per wave: the whole wave runs its stage B, as the kernel does)
+            if (lat && per == 1 && wave::readlane(res == stream::R_STAGE_B && lds_doc ? 1u : 0u, 0) != 0) {
+                auto bcast = [](const void* q) {
+                    const uint64_t v = (uint64_t)(uintptr_t)q;
+                    return (uintptr_t)((uint64_t)wave::readlane((uint32_t)v, 0) |
+                                       ((uint64_t)wave::readlane((uint32_t)(v >> 32), 0) << 32));
+                };
+                const uint8_t* d0 = reinterpret_cast<const uint8_t*>(bcast(lds_doc));
+                uint64_t* row0 = reinterpret_cast<uint64_t*>(bcast(rowp));
+                const uint64_t* dw0 = reinterpret_cast<const uint64_t*>(bcast(dwp));
+                const bool ok = stream::finish_full<true>(span, blob, d0, lens[span], RowRef(row0), out_tri, out_err,
+                                                          out_bm, stride, dw0);
+                if (l == 0) out_slow[span] = ok ? 2 : 1;
+                return;
+            }
             if (l >= per || r >= n) return;
             out_slow[r] = res == stream::R_SLOW ? 1 : 0;
             if (res == stream::R_STAGE_B && lds_doc) {  // stage B on the ring's copy of the document
