@@ -115,7 +115,8 @@ struct authjx_ctx {
     int ablate = 0;  // profiling / comparison only: 41 the lean single-pass kernel where the
                      // streaming kernel would run, 52 the streaming kernel for a one-ruleset
                      // batch of any size, 50 / 51 its structural pass alone / without its
-                     // fold, 1..3 / 10..12 token-scanner ablations and workgroup sizes
+                     // fold, 53 its small-batch phase clocks (over the bitmap), 1..3 /
+                     // 10..12 token-scanner ablations and workgroup sizes
 };
 
 namespace {
@@ -524,12 +525,12 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     for (uint32_t i = 0; i < n_sets; i++) all_stream = all_stream && sets[i]->stream_ok;
     const bool small = n <= stream_max_n;
     const bool use_stream = !force_scan && all_stream &&
-                            ((ablate == 0 && small) || (n_sets == 1 && ablate >= 50 && ablate <= 52));
+                            (((ablate == 0 || ablate == 53) && small) || (n_sets == 1 && ablate >= 50 && ablate <= 52));
     // requests per wave: 32 for throughput, fewer for a small batch (more waves share it)
     uint32_t per = ajx::kStreamSpan;
     if (n_sets > 1)
         per = 1;
-    else if (ablate == 0)
+    else if (ablate == 0 || ablate == 53)
         per = std::max<uint32_t>(1u, std::min<uint32_t>(ajx::kStreamSpan, (n + 2047u) / 2048u));
     uint32_t max_rec = 0;
     for (uint32_t i = 0; i < n_sets; i++) max_rec = std::max(max_rec, sets[i]->stream_rec);
@@ -568,7 +569,8 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         HIP_OK(ajx::launch_eval_stream(w->d_sets, d_set_of_req, (uint32_t)max_blob, max_rec, d_arena,
                                        d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap,
                                        bitmap_stride_words, w->d_rows, rows_stride, keep_rows, w->d_perm, w->d_slow,
-                                       w->d_slow + 2, s, ablate == 50 ? 1 : ablate == 51 ? 2 : 0, mods, per));
+                                       w->d_slow + 2, s, ablate == 50 ? 1 : ablate == 51 ? 2 : ablate == 53 ? 3 : 0, mods,
+                                       per));
     } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
         // caller's bucketing by AuthConfig), a full kernel, batches worth sorting

@@ -187,13 +187,27 @@ static void launch_slow_list(bool mods, uint32_t sgrid, hipStream_t stream, cons
 // patterns, literals, DFA tables, fold code — h->total_bytes, a multiple of 16) is
 // copied into dynamic LDS once per workgroup; every thread reaches the barrier. All
 // table reads of the scan and the patterns are then ds_reads.
+// copies nq 16-byte words, eight loads in flight per thread before their stores (a plain
+// loop waits for each load in turn: a load latency per iteration)
+__device__ __forceinline__ void copy_words(uint4* __restrict__ dst, const uint4* __restrict__ src, uint32_t nq,
+                                           uint32_t t, uint32_t nt) {
+    for (uint32_t b = t; b < nq; b += 8u * nt) {
+        uint4 v[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+            if (b + j * nt < nq) v[j] = src[b + j * nt];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+            if (b + j * nt < nq) dst[b + j * nt] = v[j];
+    }
+}
+
 template <bool SHARED>
 __device__ __forceinline__ const uint8_t* stage_blob(const uint8_t* gblob) {
     if constexpr (SHARED) {
         extern __shared__ uint4 s_blob[];
         const uint32_t nq = reinterpret_cast<const RulesetHdr*>(gblob)->total_bytes / 16;
-        const uint4* g = reinterpret_cast<const uint4*>(gblob);
-        for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) s_blob[i] = g[i];
+        copy_words(s_blob, reinterpret_cast<const uint4*>(gblob), nq, threadIdx.x, blockDim.x);
         __syncthreads();
         return reinterpret_cast<const uint8_t*>(s_blob);
     } else {
@@ -544,6 +558,12 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
     extern __shared__ uint4 s_stream_dyn[];
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
     const uint32_t span = blockIdx.x * (blockDim.x >> 6) + w;
+    // (profiling, keep_rows bit 1: lane 0 of a one-request wave writes its phases' clock
+    // counts over the request's bitmap word: blob copy | stream | stage B, 21 bits each, x16)
+    const bool timing = (keep_rows & 2u) != 0;
+    keep_rows &= 1u;
+    const uint64_t c0 = timing ? __builtin_readcyclecounter() : 0ull;
+    uint64_t c1 = 0, c2 = 0;
     const uint8_t* blob;
     uint8_t* base;
     if constexpr (MT) {
@@ -553,8 +573,7 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
         uint8_t* wb = reinterpret_cast<uint8_t*>(s_stream_dyn) + w * wave_bytes;
         const uint32_t tb = lean::uni(reinterpret_cast<const RulesetHdr*>(g)->total_bytes);  // (x16)
         if (tb <= wave_off) {
-            for (uint32_t i = l; i < tb / 16u; i += 64u)
-                reinterpret_cast<uint4*>(wb)[i] = reinterpret_cast<const uint4*>(g)[i];
+            copy_words(reinterpret_cast<uint4*>(wb), reinterpret_cast<const uint4*>(g), tb / 16u, l, 64u);
             wave::sync();
             blob = wb;
         } else {
@@ -568,11 +587,19 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
     stream::WaveLds& L = *reinterpret_cast<stream::WaveLds*>(base);
     uint64_t* rows = reinterpret_cast<uint64_t*>(base + sizeof(stream::WaveLds));
     if (span * per >= n) return;  // (wave-uniform)
+    if (timing) c1 = __builtin_readcyclecounter();
     const uint64_t *rowp = nullptr, *dwp = nullptr;
     const uint8_t* lds_doc = nullptr;
     const uint32_t res = stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
                                                  out_bm, stride, &rowp, &dwp, LAT ? &lds_doc : nullptr);
     const uint32_t r = span * per + l;
+    if (timing) c2 = __builtin_readcyclecounter();
+    auto times = [&](uint32_t rq) {
+        if (!timing || l != 0 || !out_bm) return;
+        const uint64_t c3 = __builtin_readcyclecounter();
+        auto f = [](uint64_t a, uint64_t b) { return ((b - a) >> 4) & 0x1FFFFFull; };
+        out_bm[(size_t)rq * stride] = f(c0, c1) | (f(c1, c2) << 21) | (f(c2, c3) << 42);
+    };
     if constexpr (LAT) {
         // one request per wave: every lane takes part in its stage B (finish_full<true>)
         if (per == 1 && wave::readlane(res == stream::R_STAGE_B && lds_doc ? 1u : 0u, 0) != 0) {
@@ -591,6 +618,7 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
                 atomicAdd(slow_count, 1u);
                 stage_ids[atomicAdd(slow_count + 1, 1u)] = r0 | kStageExact;
             }
+            times(r0);
             return;
         }
     }
@@ -699,6 +727,8 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
     if (n == 0) return hipSuccess;
     if (row_stride < 5u + n_rec) return hipErrorInvalidValue;
     const bool mt = d_set_of_req != nullptr;
+    const bool timing = mode == 3;  // (profiling: the LAT instance's phase clocks, §ajx_scan_stream)
+    if (timing) mode = 0;
     if (mt) {
         if (mode != 0) return hipErrorInvalidValue;
         per = 1;
@@ -757,7 +787,7 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
                        d_arena, \
                        d_offs, d_lens, n, \
                        d_slow_count, d_slow_ids, d_stage_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes,       \
-                       d_rows, row_stride, keep_rows ? 1u : 0u, per, merge ? 1u : 0u)
+                       d_rows, row_stride, (keep_rows ? 1u : 0u) | (timing ? 2u : 0u), per, merge ? 1u : 0u)
     const bool lat = merge && !keep_rows;
     if (mt && lat)
         AJX_STREAM_LAUNCH(0, true, true);

@@ -1054,18 +1054,24 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
             ValueRef v;
             v.type = T_NULL;
             v.start = v.end = 0;
-            bool whole = e.slot == 0xFFFFu;
-            if (!whole) {
-                const uint64_t pre = row[1u + e.slot];
+            if (e.slot == 0xFFFFu) {  // (no prefix the stream follows: the whole document)
+                v = gj_get(d, n, comps + sels[e.sel].comp_begin, sels[e.sel].comp_count, lits);
+            } else {
+                // the prefix's match is the document's only one (the stream sends a second
+                // match of a record to the exact scan), so gjson's first complete match of
+                // the whole path, if any, lies inside it
+                uint64_t pre = row[1u + e.slot];
                 if ((uint32_t)pre == kNone) continue;  // (no prefix: not found)
+                // (a prefix whose own patterns were all decided may still be open)
+                if (((pre >> 32) & kOpenEnd) && !resolve_open(d, n, (uint32_t)pre, &pre)) {
+                    bad = true;
+                    break;
+                }
                 const uint32_t a = (uint32_t)pre, len = (uint32_t)(pre >> 32) & 0xFFFFFFu;
                 v = gj_get(d + a, len, comps + e.comp_begin, e.comp_count, lits);
                 v.start += a;
                 v.end += a;
-                // (not inside the first match of the prefix: the whole document decides)
-                whole = v.type == T_NULL && v.start == v.end;
             }
-            if (whole) v = gj_get(d, n, comps + sels[e.sel].comp_begin, sels[e.sel].comp_count, lits);
             if (v.type == T_NULL && v.start == v.end) continue;  // (not found: Null)
             row[1u + e.sel] = (uint64_t)v.start |
                               ((uint64_t)(((v.end - v.start) & 0xFFFFFFu) | ((uint32_t)v.type << 24) |
@@ -1074,6 +1080,10 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
                 wave::lds_or64(&row[0], 1ull << e.sel);
             else
                 row[0] = row[0] | (1ull << e.sel);
+        }
+        if (fail_any(bad)) {
+            if (lane == 0) row[0] = kRowSlow;
+            return false;
         }
         if constexpr (WAVE) wave::sync();
     }

@@ -132,7 +132,9 @@ int authjx_init(int device, authjx_ctx** out);
 void authjx_shutdown(authjx_ctx* ctx);
 /* Release the per-stream workspace (capture rows, slow list, order, set table) the
  * context keeps for `stream` since its first device call on it, after that stream's last
- * batch: for callers that use short-lived streams. Not the context's own stream. */
+ * batch: for callers that use short-lived streams. Not the context's own stream. A call
+ * still running on that stream, or an authjx_last_* reader, keeps the workspace until it
+ * returns (reference-counted); only authjx_shutdown must not race the context's calls. */
 int authjx_release_stream(authjx_ctx* ctx, void* stream);
 // The sha256 (first 32 hex digits) of the sources the library was built from
 // (authorino_amd/build.py source_hash); the Python runtime refuses a stale binary.
@@ -249,8 +251,8 @@ int authjx_select_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint
  * pkg/evaluators/authorization.go:56-66. Request r's text slot is
  * out_text[r * text_stride, (r + 1) * text_stride); a value esc has AUTHJX_VALUE_TEXT and
  * start / len within that slot. A value that does not fit, or that the device leaves
- * undecided (non-ASCII @case / @strip), is AUTHJX_JSON_UNSUPPORTED. Plain selectors are
- * document spans as above. */
+ * undecided (@case / @strip on a code point its Unicode tables do not vouch for), is
+ * AUTHJX_JSON_UNSUPPORTED. Plain selectors are document spans as above. */
 int authjx_select_text_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
                                     const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
                                     const uint32_t* d_lens, uint32_t n, authjx_value* d_out_values,
