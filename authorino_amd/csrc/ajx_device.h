@@ -1011,15 +1011,18 @@ AJX_HD uint8_t run_fold(const uint32_t* code, uint32_t n_code, ResFn res, int32_
 // (which would live in scratch memory).
 AJX_HD uint64_t sel64(bool c, uint64_t a, uint64_t b) { return c ? a : b; }  // a value select
 
-AJX_HD uint8_t run_fold_bits(const uint32_t* code, uint32_t n_code, const uint64_t t[2], const uint64_t u[2],
-                             const uint64_t se[2], int32_t* err) {
+// fetch(k): code word k (run_fold_bits: from memory; a wave running one fold together can
+// hand out words it holds in registers)
+template <class Fetch>
+AJX_HD uint8_t run_fold_bits_f(Fetch fetch, uint32_t n_code, const uint64_t t[2], const uint64_t u[2],
+                               const uint64_t se[2], int32_t* err) {
     const uint64_t t0 = t[0], t1 = t[1], u0 = u[0], u1 = u[1], s0 = se[0], s1 = se[1];
     uint32_t kinds = 0, vals = 0;
     uint64_t ep_lo = 0, ep_hi = 0;  // levels 0..7 / 8..15
     uint32_t sp = 0;
     uint32_t out = V_T, out_e = 0;
     for (uint32_t k = 0; k < n_code; k++) {
-        const uint32_t w = code[k];
+        const uint32_t w = fetch(k);
         const uint32_t op = w >> 24, arg = w & 0xFFFFFFu;
         uint32_t v = V_T, e = 0;
         if (op == C_OPEN_AND || op == C_OPEN_OR) {
@@ -1061,6 +1064,10 @@ AJX_HD uint8_t run_fold_bits(const uint32_t* code, uint32_t n_code, const uint64
     }
     *err = (out == V_E || out == V_U) ? (int32_t)out_e - 1 : -1;
     return (uint8_t)out;
+}
+AJX_HD uint8_t run_fold_bits(const uint32_t* code, uint32_t n_code, const uint64_t t[2], const uint64_t u[2],
+                             const uint64_t se[2], int32_t* err) {
+    return run_fold_bits_f([&](uint32_t k) { return code[k]; }, n_code, t, u, se, err);
 }
 
 }  // namespace ajx

@@ -936,9 +936,9 @@ AJX_HD bool resolve_open(const uint8_t* d, uint32_t n, uint32_t a, uint64_t* rec
 // The arrays the stream compared element by element decide their selectors' incl / excl
 // patterns: dD / dT (decided, true) from the eager words dw and the row's records.
 AJX_HD void array_decisions(const EagerSel* eg, uint32_t ns, RowRef row, const uint64_t dw[4], uint64_t& dD,
-                            uint64_t& dT) {
+                            uint64_t& dT, uint32_t s0 = 0, uint32_t sstep = 1) {
     if (!eg) return;
-    for (uint32_t s = 0; s < ns && s < 32u; s++) {
+    for (uint32_t s = s0; s < ns && s < 32u; s += sstep) {
         const uint64_t rec = row[1u + s];
         const uint32_t meta = (uint32_t)(rec >> 32);
         if ((uint32_t)rec == kNone || !(meta & kOpenEnd) || !((meta >> 29) & 1u) || ((dw[3] >> s) & 1ull)) continue;
@@ -1022,7 +1022,18 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
     const uint64_t dw[4] = {dwp ? dwp[0] : row[1u + nr], dwp ? dwp[1] : row[2u + nr], dwp ? dwp[2] : row[3u + nr],
                             dwp ? dwp[3] : row[4u + nr]};
     uint64_t dD = dw[0], dT = dw[1];
-    array_decisions(eg, ns, row, dw, dD, dT);
+    array_decisions(eg, ns, row, dw, dD, dT, lane, step);
+    // (WAVE: OR over the lanes)
+    auto orall = [](uint64_t x) -> uint64_t {
+        const auto OR = [](uint32_t a, uint32_t b) { return a | b; };
+        const uint32_t lo = wave::readlane(wave::scan_incl((uint32_t)x, 0u, OR), 63);
+        const uint32_t hi = wave::readlane(wave::scan_incl((uint32_t)(x >> 32), 0u, OR), 63);
+        return (uint64_t)lo | ((uint64_t)hi << 32);
+    };
+    if constexpr (WAVE) {
+        dD = orall(dD);
+        dT = orall(dT);
+    }
     const SelectorPatterns* sps = reinterpret_cast<const SelectorPatterns*>(blob + h->off_sel_patterns);
     bool bad = false;
     for (uint32_t s = lane; s < nr; s += step) {
@@ -1091,12 +1102,6 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
     const uint64_t dec[2] = {dD, dT};
     patterns_from_row(blob, d, row, t, u, dec, lane, step);
     if constexpr (WAVE) {  // (OR over the lanes)
-        auto orall = [](uint64_t x) -> uint64_t {
-            const auto OR = [](uint32_t a, uint32_t b) { return a | b; };
-            const uint32_t lo = wave::readlane(wave::scan_incl((uint32_t)x, 0u, OR), 63);
-            const uint32_t hi = wave::readlane(wave::scan_incl((uint32_t)(x >> 32), 0u, OR), 63);
-            return (uint64_t)lo | ((uint64_t)hi << 32);
-        };
         t[0] = orall(t[0]);
         t[1] = orall(t[1]);
         u[0] = orall(u[0]);
@@ -1106,8 +1111,7 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
         if (lane == 0) row[0] = kRowSlow;
         return false;
     }
-    if (lane != 0) return true;
-    if (out_bm) {
+    if (lane == 0 && out_bm) {
         uint64_t* orow = out_bm + (size_t)r * stride;
         orow[0] = t[0];
         if (stride > 1) orow[1] = t[1];
@@ -1116,17 +1120,41 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
     const uint64_t se[2] = {h->static_error[0], h->static_error[1]};
     const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
     const uint32_t nt = h->pad1[0];
+    // WAVE: every lane runs the (uniform) fold, its code words handed out from registers
+    // (64 per coalesced read) instead of one dependent memory read each
+    auto fold = [&](const uint32_t* c, uint32_t nc, int32_t* ep) -> uint8_t {
+        if constexpr (WAVE) {
+            uint32_t creg = 0, cbase = 0xFFFFFFFFu;
+            return run_fold_bits_f(
+                [&](uint32_t k) -> uint32_t {
+                    const uint32_t b = k & ~63u;
+                    if (b != cbase) {
+                        cbase = b;
+                        creg = b + lane < nc ? c[b + lane] : 0u;
+                    }
+                    return wave::readlane(creg, k & 63u);
+                },
+                nc, t, u, se, ep);
+        }
+        return run_fold_bits(c, nc, t, u, se, ep);
+    };
     if (nt == 0) {
         int32_t ep;
-        out_tri[r] = run_fold_bits(code, h->n_code, t, u, se, &ep);
-        if (out_err) out_err[r] = ep;
+        const uint8_t v = fold(code, h->n_code, &ep);
+        if (lane == 0) {
+            out_tri[r] = v;
+            if (out_err) out_err[r] = ep;
+        }
         return true;
     }
     const uint32_t* rc = reinterpret_cast<const uint32_t*>(blob + h->pad1[1]);
     for (uint32_t k = 0; k < nt; k++) {
         int32_t ep;
-        out_tri[(size_t)r * nt + k] = run_fold_bits(code + rc[2 * k], rc[2 * k + 1], t, u, se, &ep);
-        if (out_err) out_err[(size_t)r * nt + k] = ep;
+        const uint8_t v = fold(code + rc[2 * k], rc[2 * k + 1], &ep);
+        if (lane == 0) {
+            out_tri[(size_t)r * nt + k] = v;
+            if (out_err) out_err[(size_t)r * nt + k] = ep;
+        }
     }
     return true;
 }

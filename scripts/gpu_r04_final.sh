@@ -1,7 +1,6 @@
-# round 4 evidence on the final tree: HBM traffic passes (FETCH_SIZE / WRITE_SIZE, one
-# counter per pass) of the dominant kernel per workload -> pmc_traffic.json, the SQ mix of
-# c2 and c3, the streaming kernel's SQ mix on c2 (kernel modes 50 / 52), the GPU suite, the
-# bench lines c2..c5 (CPU baseline, parity), rocprofv3 stats, smoke
+# round 4 evidence, part 1: HBM traffic passes (FETCH_SIZE / WRITE_SIZE, one counter per
+# pass) of the dominant kernel per workload -> pmc_traffic.json, the SQ mix of c2 and c3,
+# the streaming kernel's SQ mix on c2 (kernel modes 50 / 52); part 2: gpu_r04_final2.sh
 R=$GRAFT_REPO_ROOT; cd $R && O=gpurun_out/${OUT:-r04final} && mkdir -p $O && export TMPDIR=/tmp
 ns() { case $1 in c4|c5) echo 2097152;; *) echo 1048576;; esac; }
 for w in ${WLS:-c2 c3 c4 c5}; do
@@ -18,19 +17,5 @@ for m in 50 52; do
   (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d $R/$O/pmc_sq_stream_m$m -o run -- python3 $R/bench.py --no-cpu --no-pcie --no-serve --workload c2 --steps 2 --warmup 1 --kernel-mode $m > $R/$O/pmc_sq_stream_m$m.log 2>&1) || { echo "pmc sq stream $m failed"; exit 1; }
 done
 python3 scripts/pmc_summary.py $O/pmc_sq_c2 $O/pmc_sq_c3 $O/pmc_sq_stream_m50 $O/pmc_sq_stream_m52 > $O/pmc_sq.txt 2>&1
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
-tail -3 $O/pytest_gpu.log; grep -E "FAILED|ERROR" $O/pytest_gpu.log | head -20 || true
-[ $rc -le 1 ] || { echo "pytest rc=$rc"; exit 1; }
-for w in c2 c3 c4 c5; do
-  timeout -k 10 500 python -u bench.py --workload $w > $O/bench_$w.log 2>&1 || { echo "bench $w failed"; tail -20 $O/bench_$w.log; exit 1; }
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_$w -o $w -- python3 $R/bench.py --no-cpu --no-pcie --no-serve --workload $w --steps 5 > $R/$O/prof_$w.log 2>&1) || echo "rocprof $w failed"
-done
-(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_n64 -o n64 -- python3 $R/bench.py --no-cpu --no-pcie --no-serve --workload c2 --n 64 --steps 50 > $R/$O/prof_n64.log 2>&1) || echo "rocprof n64 failed"
-grep -h '"metric"' $O/bench_*.log | python3 -c "
-import sys, json
-for l in sys.stdin:
-    d = json.loads(l); print(d['config'].get('workload'), round(d['ms_per_step'],3), round(d['roofline']['kernel_ms'],3), round(d['roofline']['frac'],4), d['roofline'].get('traffic'), d.get('parity'), d.get('exact_path_requests'), d.get('undecided'), (d.get('cpu_baseline') or {}).get('value'))
-    for s in d.get('serving') or []: print('   serving', s.get('producer_threads'), s.get('window_us'), s.get('latency_us'), round(s.get('decisions_per_s')))"
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo smoke ok || echo smoke failed
 cp pmc_traffic.json $O/pmc_traffic.json
 echo done
