@@ -71,7 +71,7 @@ struct Workspace {
     bool sets_ev_rec[2] = {false, false};
     std::vector<const uint8_t*> last_sets;
     // [0] = count, [1..] = ids: requests for the exact scan (the streaming kernel: [1] its
-    // stage-B count, ids from [2])
+    // stage-B count, [2] its finished waves, ids from [3])
     uint32_t* d_slow = nullptr;
     uint32_t slow_cap = 0;
     uint64_t* d_rows = nullptr;  // stage-A capture rows
@@ -265,7 +265,7 @@ int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
         if (w->d_slow) (void)hipFree(w->d_slow);
         w->d_slow = nullptr;
         w->slow_cap = 0;
-        HIP_OK(hipMalloc(&w->d_slow, ((size_t)n + 2) * sizeof(uint32_t)));
+        HIP_OK(hipMalloc(&w->d_slow, ((size_t)n + 3) * sizeof(uint32_t)));
         w->slow_cap = n;
     }
     if (n > w->perm_cap) {
@@ -569,7 +569,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
         HIP_OK(ajx::launch_eval_stream(w->d_sets, d_set_of_req, (uint32_t)max_blob, max_rec, d_arena,
                                        d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap,
                                        bitmap_stride_words, w->d_rows, rows_stride, keep_rows, w->d_perm, w->d_slow,
-                                       w->d_slow + 2, s, ablate == 50 ? 1 : ablate == 51 ? 2 : ablate == 53 ? 3 : 0, mods,
+                                       w->d_slow + 3, s, ablate == 50 ? 1 : ablate == 51 ? 2 : ablate == 53 ? 3 : 0, mods,
                                        per));
     } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the

@@ -57,7 +57,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
 // says whether it can take the ruleset. d_rows: rows of row_stride >= 5 + n_rec
 // words for n requests (wave layout, work-item = request): the rows stage B reads, and with
 // keep_rows every request's row for authjx_select_from_eval_device. d_stage_ids: n u32;
-// d_slow_count[1] (the stage-B count) follows the slow count. mode (profiling): 1 the structural pass alone, 2 no fold. per: requests per wave
+// d_slow_count[1] (the stage-B count) and [2] (finished waves) follow the slow count. mode (profiling): 1 the structural pass alone, 2 no fold. per: requests per wave
 // (1..32, 0 = 32): fewer for small batches, so more waves share the walk. d_set_of_req
 // (a multi-tenant batch, every ruleset stream-eligible): one request per wave under its
 // own ruleset, tables from global memory; n_rec then the largest of the batch.

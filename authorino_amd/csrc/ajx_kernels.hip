@@ -543,7 +543,7 @@ constexpr uint32_t kStageExact = 1u << 31;
 // still, and its lanes run stage B there (finish_full on the ring); what that leaves goes
 // to the exact scan through the stage-B list.
 template <int MODE, bool MT = false, bool LAT = false>
-__global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __restrict__ sets,
+__device__ __forceinline__ void stream_body(const uint8_t* const* __restrict__ sets,
                                                        const uint32_t* __restrict__ set_of_req,
                                                        const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ offs,
@@ -660,6 +660,51 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
     }
 }
 
+// The kernel: the span's walk (stream_body), then, with FIN (a small batch without
+// modifier chains), the stage-B list in the wave that finishes last: the requests left to
+// the exact scan and those whose stage B could not run on the LDS copy — no second launch.
+// slow_count[2] counts the finished waves.
+template <int MODE, bool MT = false, bool LAT = false, bool FIN = false>
+__global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __restrict__ sets,
+                                                       const uint32_t* __restrict__ set_of_req,
+                                                       const uint8_t* __restrict__ arena,
+                                                       const uint64_t* __restrict__ offs,
+                                                       const uint32_t* __restrict__ lens, uint32_t n,
+                                                       uint32_t* __restrict__ slow_count,
+                                                       uint32_t* __restrict__ slow_ids, uint32_t* __restrict__ stage_ids,
+                                                       uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                                       uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t wave_off,
+                                                       uint32_t wave_bytes, uint64_t* __restrict__ rows_out,
+                                                       uint32_t row_stride, uint32_t keep_rows, uint32_t per,
+                                                       uint32_t merge_slow) {
+    stream_body<MODE, MT, LAT>(sets, set_of_req, arena, offs, lens, n, slow_count, slow_ids, stage_ids, out_tri,
+                               out_err, out_bm, stride, wave_off, wave_bytes, rows_out, row_stride, keep_rows, per,
+                               merge_slow);
+    if constexpr (FIN) {
+        const uint32_t l = threadIdx.x & 63u;
+        __threadfence();  // (this wave's stage-B list entries and rows, before its count)
+        uint32_t last = 0;
+        if (l == 0) last = atomicAdd(slow_count + 2, 1u) + 1u == gridDim.x * (blockDim.x >> 6) ? 1u : 0u;
+        if (!wave::readlane(last, 0)) return;
+        __threadfence();
+        const uint32_t cnt = __hip_atomic_load(slow_count + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t i = l; i < cnt; i += 64u) {
+            const uint32_t e = stage_ids[i];
+            const uint32_t r = e & ~kStageExact;
+            const uint8_t* blob = sets[MT ? set_of_req[r] : 0];
+            bool ok = false;
+            if (!(e & kStageExact)) {
+                ok = stream::finish_full(r, blob, arena + offs[r], lens[r], wave_row(rows_out, row_stride, r), out_tri,
+                                         out_err, out_bm, stride);
+                if (!ok) atomicAdd(slow_count, 1u);
+            }
+            if (!ok)
+                eval_scan_one<false>(r, sets, MT ? set_of_req : nullptr, arena, offs, lens, out_tri, out_err, out_bm,
+                                     stride, nullptr);
+        }
+    }
+}
+
 // Stage B of the streaming kernel: one work-item per request on the stage-B list, on its
 // row in HBM (stream::finish_full); what it can not decide goes to the slow list. MT: each
 // request's own ruleset, read from global memory. EXACT (small batches, one launch fewer):
@@ -754,8 +799,8 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
     const bool merge = mt || per < stream::kSpan;
     const uint32_t spans = (n + per - 1) / per;
     const uint32_t grid = (spans + block / 64 - 1) / (block / 64);
-    // (one fill: the slow count and the stage-B count after it)
-    hipError_t e = hipMemsetAsync(d_slow_count, 0, 2 * sizeof(uint32_t), stream);
+    // (one fill: the slow count, the stage-B count and the finished-wave count after it)
+    hipError_t e = hipMemsetAsync(d_slow_count, 0, 3 * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     static std::atomic<uint64_t> attr_done{0};
     e = attr_once(attr_done, [] {
@@ -765,6 +810,8 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
                               reinterpret_cast<const void*>(&ajx_scan_stream<0, true>),
                               reinterpret_cast<const void*>(&ajx_scan_stream<0, false, true>),
                               reinterpret_cast<const void*>(&ajx_scan_stream<0, true, true>),
+                              reinterpret_cast<const void*>(&ajx_scan_stream<0, false, true, true>),
+                              reinterpret_cast<const void*>(&ajx_scan_stream<0, true, true, true>),
                               reinterpret_cast<const void*>(&ajx_stream_finish<false>),
                               reinterpret_cast<const void*>(&ajx_stream_finish<false, 1>),
                               reinterpret_cast<const void*>(&ajx_stream_finish<false, 2>),
@@ -782,28 +829,33 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
         return hipSuccess;
     });
     if (e != hipSuccess) return e;
-#define AJX_STREAM_LAUNCH(M, T, LT)                                                                           \
-    hipLaunchKernelGGL((ajx_scan_stream<M, T, LT>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,     \
+#define AJX_STREAM_LAUNCH(M, T, LT, F)                                                                        \
+    hipLaunchKernelGGL((ajx_scan_stream<M, T, LT, F>), dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,  \
                        d_arena, \
                        d_offs, d_lens, n, \
                        d_slow_count, d_slow_ids, d_stage_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes,       \
                        d_rows, row_stride, (keep_rows ? 1u : 0u) | (timing ? 2u : 0u), per, merge ? 1u : 0u)
     const bool lat = merge && !keep_rows;
-    if (mt && lat)
-        AJX_STREAM_LAUNCH(0, true, true);
+    const bool fin = lat && !mods;  // (stage B and the exact scan in the last wave: no second launch)
+    if (mt && fin)
+        AJX_STREAM_LAUNCH(0, true, true, true);
+    else if (mt && lat)
+        AJX_STREAM_LAUNCH(0, true, true, false);
     else if (mt)
-        AJX_STREAM_LAUNCH(0, true, false);
+        AJX_STREAM_LAUNCH(0, true, false, false);
     else if (mode == 1)
-        AJX_STREAM_LAUNCH(1, false, false);
+        AJX_STREAM_LAUNCH(1, false, false, false);
     else if (mode == 2)
-        AJX_STREAM_LAUNCH(2, false, false);
+        AJX_STREAM_LAUNCH(2, false, false, false);
+    else if (fin)
+        AJX_STREAM_LAUNCH(0, false, true, true);
     else if (lat)
-        AJX_STREAM_LAUNCH(0, false, true);
+        AJX_STREAM_LAUNCH(0, false, true, false);
     else
-        AJX_STREAM_LAUNCH(0, false, false);
+        AJX_STREAM_LAUNCH(0, false, false, false);
 #undef AJX_STREAM_LAUNCH
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (mode != 0) return hipSuccess;
+    if (mode != 0 || fin) return hipSuccess;
     // stage B and the exact scan over their lists (grid-stride: the lists' lengths are on the device)
     const uint32_t fgrid = n < 2048u * 256u ? (n + 255) / 256 : 4096;
 #define AJX_FINISH_LAUNCH(T, X, LDS)                                                                              \
