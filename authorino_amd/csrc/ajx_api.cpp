@@ -74,6 +74,9 @@ struct Workspace {
     // stage-B count, [2] its finished waves, ids from [3])
     uint32_t* d_slow = nullptr;
     uint32_t slow_cap = 0;
+    // the streaming kernel's small-batch instance (FIN) leaves [0..2] zero for the next launch
+    // on this stream (no fill) and publishes its exact-path count at [3]
+    bool cnt_zero = false, exact3 = false;
     uint64_t* d_rows = nullptr;  // stage-A capture rows
     size_t rows_cap = 0;         // in u64
     uint32_t* d_perm = nullptr;  // length-bucketed request order (+ 2 x 1024 + 1 u32 histogram)
@@ -217,11 +220,19 @@ void retire_stream(authjx_ctx* ctx, hipStream_t s) {
     if (dead) destroy_workspace(w);  // (else the call still on that stream does, when it ends)
 }
 
-int ensure_sets(Workspace* w, int device, const authjx_ruleset* const* sets, uint32_t n_sets) {
+// d_pre: the caller's device copy of the blob pointers (the micro-batcher's staging buffer,
+// one copy with the documents), used as is
+int ensure_sets(Workspace* w, int device, const authjx_ruleset* const* sets, uint32_t n_sets,
+                const uint8_t* const* d_pre = nullptr) {
     std::vector<const uint8_t*> ptrs(n_sets);
     for (uint32_t i = 0; i < n_sets; i++) {
         if (!sets[i] || sets[i]->device != device) return AUTHJX_EINVAL;
         ptrs[i] = sets[i]->d_blob;
+    }
+    if (d_pre) {
+        w->d_sets = const_cast<const uint8_t**>(d_pre);
+        w->last_sets.clear();  // (the next call without one copies its table again)
+        return AUTHJX_OK;
     }
     if (ptrs == w->last_sets) return AUTHJX_OK;
     if (n_sets > w->sets_cap) {  // (grows: the stream's previous batches may read the old table)
@@ -265,8 +276,9 @@ int ensure_work(Workspace* w, uint32_t n, uint32_t row_stride) {
         if (w->d_slow) (void)hipFree(w->d_slow);
         w->d_slow = nullptr;
         w->slow_cap = 0;
-        HIP_OK(hipMalloc(&w->d_slow, ((size_t)n + 3) * sizeof(uint32_t)));
+        HIP_OK(hipMalloc(&w->d_slow, ((size_t)n + 4) * sizeof(uint32_t)));
         w->slow_cap = n;
+        w->cnt_zero = w->exact3 = false;
     }
     if (n > w->perm_cap) {
         if (w->d_perm) (void)hipFree(w->d_perm);
@@ -484,10 +496,13 @@ size_t authjx_pattern_error(const authjx_ruleset* rs, uint32_t i, char* buf, siz
     return e.size();
 }
 
-int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
-                             const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
-                             const uint32_t* d_lens, uint32_t n, uint8_t* d_out_tristate, int32_t* d_out_err_idx,
-                             uint64_t* d_out_bitmap, uint32_t bitmap_stride_words, void* stream) {
+// authjx_eval_batch_device; d_sets_pre: the blob pointers already on the device (the
+// micro-batcher's one staging copy), else this stream's table is filled from sets
+static int eval_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                       const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
+                       const uint32_t* d_lens, uint32_t n, uint8_t* d_out_tristate, int32_t* d_out_err_idx,
+                       uint64_t* d_out_bitmap, uint32_t bitmap_stride_words, void* stream,
+                       const uint8_t* const* d_sets_pre) {
     if (!ctx || !sets || n_sets == 0 || (n && (!d_arena || !d_offs || !d_lens || !d_out_tristate)))
         return AUTHJX_EINVAL;
     if (n_sets > 1 && !d_set_of_req) return AUTHJX_EINVAL;
@@ -516,7 +531,7 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     if (!w) return AUTHJX_EDEVICE;
     hipStream_t s = w->stream;
     HIP_OK(hipSetDevice(ctx->device));
-    int rc = ensure_sets(w, ctx->device, sets, n_sets);
+    int rc = ensure_sets(w, ctx->device, sets, n_sets, d_sets_pre);
     if (rc != AUTHJX_OK) return rc;
     // the streaming kernel: small batches (latency; one request per wave for a multi-tenant
     // batch) whose rulesets all have stream tables; any one-ruleset batch under kernel
@@ -559,6 +574,9 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
     w->rows_wave = true;
     size_t max_blob = 0;
     for (uint32_t i = 0; i < n_sets; i++) max_blob = std::max(max_blob, sets[i]->c.blob.size());
+    // (the counters are zero only after a FIN launch: every other launch fills them itself)
+    bool cnt_zero = w->cnt_zero;
+    w->cnt_zero = w->exact3 = false;
     if (force_scan) {
         HIP_OK(ajx::launch_eval_scan(w->d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate,
                                      d_out_err_idx, d_out_bitmap, bitmap_stride_words, s, mods));
@@ -570,7 +588,8 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
                                        d_offs, d_lens, n, d_out_tristate, d_out_err_idx, d_out_bitmap,
                                        bitmap_stride_words, w->d_rows, rows_stride, keep_rows, w->d_perm, w->d_slow,
                                        w->d_slow + 3, s, ablate == 50 ? 1 : ablate == 51 ? 2 : ablate == 53 ? 3 : 0, mods,
-                                       per));
+                                       per, &cnt_zero));
+        w->cnt_zero = w->exact3 = cnt_zero;
     } else {
         // length-bucketed order: one ruleset for the batch (multi-tenant batches keep the
         // caller's bucketing by AuthConfig), a full kernel, batches worth sorting
@@ -591,6 +610,14 @@ int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets,
                                      ablate < 20 ? ablate : 0, perm, mods));
     }
     return batch_done(w, sets, n_sets);
+}
+
+int authjx_eval_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32_t n_sets,
+                             const uint32_t* d_set_of_req, const uint8_t* d_arena, const uint64_t* d_offs,
+                             const uint32_t* d_lens, uint32_t n, uint8_t* d_out_tristate, int32_t* d_out_err_idx,
+                             uint64_t* d_out_bitmap, uint32_t bitmap_stride_words, void* stream) {
+    return eval_device(ctx, sets, n_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_out_tristate, d_out_err_idx,
+                       d_out_bitmap, bitmap_stride_words, stream, nullptr);
 }
 
 static_assert(sizeof(authjx_value) == 12, "authjx_value is three u32 words on the device");
@@ -633,6 +660,7 @@ int authjx_select_text_batch_device(authjx_ctx* ctx, const authjx_ruleset* const
     if (rc != AUTHJX_OK) return rc;
     const bool exact = force_scan != 0;  // the exact Get per selector (cross-check)
     w->rows_rs = nullptr;  // (the rows are rewritten for this ruleset)
+    w->cnt_zero = w->exact3 = false;  // (its slow count is filled and left nonzero)
     if (!exact && (rc = ensure_work(w, n, row_stride)) != AUTHJX_OK) return rc;
     const uint32_t* perm = nullptr;
     if (!exact && len_sort && n_sets == 1 && n >= 4096) {
@@ -791,7 +819,7 @@ int64_t authjx_last_exact_count(authjx_ctx* ctx) {
     if (!w->d_slow || !w->ran) return -1;
     uint32_t c = 0;
     if (hipSetDevice(ctx->device) != hipSuccess || hipEventSynchronize(w->ev1) != hipSuccess ||
-        hipMemcpy(&c, w->d_slow, sizeof c, hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(&c, w->d_slow + (w->exact3 ? 3 : 0), sizeof c, hipMemcpyDeviceToHost) != hipSuccess)
         return AUTHJX_EDEVICE;
     return (int64_t)c;
 }
@@ -863,21 +891,30 @@ int authjx_eval_batch(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint32
 
 }  // extern "C"
 
-constexpr uint32_t kBatcherWorkers = 2;  // one packs and launches while the other's batch runs
+constexpr uint32_t kBatcherMaxWorkers = 8;
+// workers per batcher: 2 by default (one packs and launches while the other's batch runs);
+// authjx_debug_batcher_workers changes it for batchers created afterwards
+std::atomic<uint32_t> g_batcher_workers{2};
 
 struct authjx_batcher {
     authjx_ctx* ctx = nullptr;
     // per worker: its own stream (its own workspace in ctx) and staging buffers
     struct Lane {
         hipStream_t stream = nullptr;
-        uint8_t* h_buf = nullptr;  // pinned staging: arena | offs | lens | set_of_req | outputs
+        uint8_t* h_buf = nullptr;  // pinned staging: arena | offs | lens | set_of_req | sets | outputs
+        uint8_t* h_dev = nullptr;  // its device address (the kernel writes the outputs there)
         size_t h_cap = 0;
         uint8_t* d_buf = nullptr;
         size_t d_cap = 0;
-    } lanes[kBatcherWorkers];
+    } lanes[kBatcherMaxWorkers];
+    uint32_t n_lanes = 2;
     ajx::BatchCore* core = nullptr;
 
-    // one batch (ordered by ruleset): pack, one launch, outputs back (worker `wid` only)
+    // one batch (ordered by ruleset): pack, one copy in, one launch (worker `wid` only).
+    // The staging copy carries the documents, offsets, lengths, each request's ruleset
+    // index and the rulesets' blob pointers; the kernel writes the results into the pinned
+    // buffer itself (mapped host memory: no copy back), so a small batch is one copy, one
+    // kernel (its counters left zero by the last one on this stream) and a synchronize.
     int evaluate(std::vector<ajx::BatchReq*>& reqs, uint32_t wid) {
         Lane& L = lanes[wid];
         hipStream_t stream = L.stream;
@@ -898,7 +935,9 @@ struct authjx_batcher {
         const size_t o_offs = round_up(arena_len + 1, 256);
         const size_t o_lens = round_up(o_offs + (size_t)n * 8, 256);
         const size_t o_sor = round_up(o_lens + (size_t)n * 4, 256);
-        const size_t o_tri = round_up(o_sor + (size_t)n * 4, 256);
+        const size_t o_sets = round_up(o_sor + (size_t)n * 4, 256);
+        const size_t o_in_end = round_up(o_sets + sets.size() * sizeof(uint8_t*), 256);
+        const size_t o_tri = o_in_end;  // (host side only: written by the kernel)
         const size_t o_err = round_up(o_tri + (size_t)n * nt, 256);
         const size_t total = round_up(o_err + (size_t)n * nt * 4, 256);
         HIP_OK(hipSetDevice(ctx->device));
@@ -906,15 +945,19 @@ struct authjx_batcher {
             if (h_buf) (void)hipHostFree(h_buf);
             h_buf = nullptr;
             h_cap = 0;
+            L.h_dev = nullptr;
             HIP_OK(hipHostMalloc(&h_buf, total, hipHostMallocDefault));
             h_cap = total;
+            void* dp = nullptr;
+            HIP_OK(hipHostGetDevicePointer(&dp, h_buf, 0));
+            L.h_dev = (uint8_t*)dp;
         }
-        if (total > d_cap) {
+        if (o_in_end > d_cap) {
             if (d_buf) (void)hipFree(d_buf);
             d_buf = nullptr;
             d_cap = 0;
-            HIP_OK(hipMalloc(&d_buf, total));
-            d_cap = total;
+            HIP_OK(hipMalloc(&d_buf, o_in_end));
+            d_cap = o_in_end;
         }
         uint64_t* offs = (uint64_t*)(h_buf + o_offs);
         uint32_t* lens = (uint32_t*)(h_buf + o_lens);
@@ -927,13 +970,14 @@ struct authjx_batcher {
         }
         h_buf[at] = 0;
         std::memcpy(h_buf + o_sor, sor.data(), (size_t)n * 4);
-        HIP_OK(hipMemcpyAsync(d_buf, h_buf, o_tri, hipMemcpyHostToDevice, stream));
-        const int rc = authjx_eval_batch_device(ctx, sets.data(), (uint32_t)sets.size(),
-                                                (const uint32_t*)(d_buf + o_sor), d_buf,
-                                                (const uint64_t*)(d_buf + o_offs), (const uint32_t*)(d_buf + o_lens),
-                                                n, d_buf + o_tri, (int32_t*)(d_buf + o_err), nullptr, 0, stream);
+        const uint8_t** hs = (const uint8_t**)(h_buf + o_sets);
+        for (size_t k = 0; k < sets.size(); k++) hs[k] = sets[k] ? sets[k]->d_blob : nullptr;
+        HIP_OK(hipMemcpyAsync(d_buf, h_buf, o_in_end, hipMemcpyHostToDevice, stream));
+        const int rc = eval_device(ctx, sets.data(), (uint32_t)sets.size(), (const uint32_t*)(d_buf + o_sor), d_buf,
+                                   (const uint64_t*)(d_buf + o_offs), (const uint32_t*)(d_buf + o_lens), n,
+                                   L.h_dev + o_tri, (int32_t*)(L.h_dev + o_err), nullptr, 0, stream,
+                                   (const uint8_t* const*)(d_buf + o_sets));
         if (rc != AUTHJX_OK) return rc;
-        HIP_OK(hipMemcpyAsync(h_buf + o_tri, d_buf + o_tri, total - o_tri, hipMemcpyDeviceToHost, stream));
         HIP_OK(hipStreamSynchronize(stream));
         const uint8_t* tri = h_buf + o_tri;
         const int32_t* err = (const int32_t*)(h_buf + o_err);
@@ -956,8 +1000,9 @@ int authjx_batcher_create(authjx_ctx* ctx, uint32_t max_batch, uint32_t window_u
     HIP_OK(hipSetDevice(ctx->device));
     authjx_batcher* b = new authjx_batcher();
     b->ctx = ctx;
-    for (auto& L : b->lanes)
-        if (hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) != hipSuccess) {
+    b->n_lanes = std::min<uint32_t>(std::max<uint32_t>(g_batcher_workers.load(), 1u), kBatcherMaxWorkers);
+    for (uint32_t k = 0; k < b->n_lanes; k++)
+        if (hipStreamCreateWithFlags(&b->lanes[k].stream, hipStreamNonBlocking) != hipSuccess) {
             for (auto& M : b->lanes)
                 if (M.stream) (void)hipStreamDestroy(M.stream);
             delete b;
@@ -965,12 +1010,20 @@ int authjx_batcher_create(authjx_ctx* ctx, uint32_t max_batch, uint32_t window_u
         }
     b->core = new ajx::BatchCore(
         max_batch, (uint64_t)window_us * 1000ull, queue_cap ? queue_cap : 4 * max_batch,
-        [b](std::vector<ajx::BatchReq*>& reqs, uint32_t wid) { return b->evaluate(reqs, wid); }, kBatcherWorkers);
+        [b](std::vector<ajx::BatchReq*>& reqs, uint32_t wid) { return b->evaluate(reqs, wid); }, b->n_lanes);
     {
         std::lock_guard<std::mutex> g(ctx->mu);
         ctx->batchers.push_back(b);
     }
     *out = b;
+    return AUTHJX_OK;
+}
+
+// Profiling only (not in authjx.h): worker threads (each with its own stream) of the
+// batchers created after this call (1..8; default 2)
+int authjx_debug_batcher_workers(uint32_t n) {
+    if (n == 0 || n > kBatcherMaxWorkers) return AUTHJX_EINVAL;
+    g_batcher_workers.store(n);
     return AUTHJX_OK;
 }
 

@@ -57,7 +57,9 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
 // says whether it can take the ruleset. d_rows: rows of row_stride >= 5 + n_rec
 // words for n requests (wave layout, work-item = request): the rows stage B reads, and with
 // keep_rows every request's row for authjx_select_from_eval_device. d_stage_ids: n u32;
-// d_slow_count[1] (the stage-B count) and [2] (finished waves) follow the slow count. mode (profiling): 1 the structural pass alone, 2 no fold. per: requests per wave
+// d_slow_count[1] (the stage-B count) and [2] (finished waves) follow the slow count;
+// counters_zero (in): [0..2] are zero already, no fill; (out): this launch leaves them zero
+// (the small-batch instance: its last wave clears them, the slow count moved to [3]). mode (profiling): 1 the structural pass alone, 2 no fold. per: requests per wave
 // (1..32, 0 = 32): fewer for small batches, so more waves share the walk. d_set_of_req
 // (a multi-tenant batch, every ruleset stream-eligible): one request per wave under its
 // own ruleset, tables from global memory; n_rec then the largest of the batch.
@@ -70,7 +72,7 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
                               uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                               uint32_t row_stride, bool keep_rows, uint32_t* d_stage_ids, uint32_t* d_slow_count,
                               uint32_t* d_slow_ids, hipStream_t stream, int mode = 0, bool mods = false,
-                              uint32_t per = 0);
+                              uint32_t per = 0, bool* counters_zero = nullptr);
 
 // Length-bucketed request order for the single-pass kernel: d_perm[n] = request ids,
 // longest 8-byte length class first; d_hist needs 2 * 1024 + 1 u32 of scratch.

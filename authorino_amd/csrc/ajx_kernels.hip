@@ -702,6 +702,15 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
                 eval_scan_one<false>(r, sets, MT ? set_of_req : nullptr, arena, offs, lens, out_tri, out_err, out_bm,
                                      stride, nullptr);
         }
+        // every other wave is done with the counters: back to zero for the next launch on
+        // this stream (no fill before it), the slow count kept at [3] for the host
+        __threadfence();
+        if (l == 0) {
+            slow_count[3] = __hip_atomic_load(slow_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            slow_count[0] = 0;
+            slow_count[1] = 0;
+            slow_count[2] = 0;
+        }
     }
 }
 
@@ -768,7 +777,10 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
                               uint32_t n_rec, const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                               uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                               uint32_t row_stride, bool keep_rows, uint32_t* d_stage_ids, uint32_t* d_slow_count,
-                              uint32_t* d_slow_ids, hipStream_t stream, int mode, bool mods, uint32_t per) {
+                              uint32_t* d_slow_ids, hipStream_t stream, int mode, bool mods, uint32_t per,
+                              bool* counters_zero) {
+    const bool was_zero = counters_zero && *counters_zero;
+    if (counters_zero) *counters_zero = false;
     if (n == 0) return hipSuccess;
     if (row_stride < 5u + n_rec) return hipErrorInvalidValue;
     const bool mt = d_set_of_req != nullptr;
@@ -799,9 +811,10 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
     const bool merge = mt || per < stream::kSpan;
     const uint32_t spans = (n + per - 1) / per;
     const uint32_t grid = (spans + block / 64 - 1) / (block / 64);
-    // (one fill: the slow count, the stage-B count and the finished-wave count after it)
-    hipError_t e = hipMemsetAsync(d_slow_count, 0, 3 * sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
+    // (one fill: the slow count, the stage-B count and the finished-wave count after it;
+    // none after a FIN launch on this stream, whose last wave cleared them)
+    hipError_t e = hipSuccess;
+    if (!was_zero && (e = hipMemsetAsync(d_slow_count, 0, 3 * sizeof(uint32_t), stream)) != hipSuccess) return e;
     static std::atomic<uint64_t> attr_done{0};
     e = attr_once(attr_done, [] {
         for (const void* k : {reinterpret_cast<const void*>(&ajx_scan_stream<0>),
@@ -855,6 +868,7 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
         AJX_STREAM_LAUNCH(0, false, false, false);
 #undef AJX_STREAM_LAUNCH
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (counters_zero) *counters_zero = fin && (mt || (mode != 1 && mode != 2));
     if (mode != 0 || fin) return hipSuccess;
     // stage B and the exact scan over their lists (grid-stride: the lists' lengths are on the device)
     const uint32_t fgrid = n < 2048u * 256u ? (n + 255) / 256 : 4096;

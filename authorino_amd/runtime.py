@@ -517,10 +517,21 @@ class Batcher:
     buckets) and evaluates each with one launch on its own stream. ctypes releases the
     GIL around the blocking call, so Python threads wait concurrently."""
 
-    def __init__(self, ctx: "Context", max_batch: int = 4096, window_us: int = 200, queue_cap: int = 0):
+    def __init__(self, ctx: "Context", max_batch: int = 4096, window_us: int = 200, queue_cap: int = 0,
+                 workers: int = 0):
+        """workers: worker threads, each with its own stream (0: the library's default, 2;
+        profiling knob, authjx_debug_batcher_workers, not part of authjx.h)."""
         L = load_library()
+        if workers:
+            L.authjx_debug_batcher_workers.argtypes = [C.c_uint32]
+            _check(L.authjx_debug_batcher_workers(int(workers)), "authjx_debug_batcher_workers")
         h = C.c_void_p()
-        _check(L.authjx_batcher_create(ctx._h, max_batch, window_us, queue_cap, C.byref(h)), "authjx_batcher_create")
+        try:
+            _check(L.authjx_batcher_create(ctx._h, max_batch, window_us, queue_cap, C.byref(h)),
+                   "authjx_batcher_create")
+        finally:
+            if workers:
+                L.authjx_debug_batcher_workers(2)
         self.ctx = ctx
         self._h = h
         ctx._batchers.add(self)

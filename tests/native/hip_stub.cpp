@@ -37,6 +37,10 @@ hipError_t hipFree(void* p) {
 }
 hipError_t hipHostMallocRaw(void** p, size_t n, unsigned) { return hipMallocRaw(p, n); }
 hipError_t hipHostFree(void* p) { return hipFree(p); }
+hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned) {
+    *d = h;
+    return hipSuccess;
+}
 hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) {
     if (n) std::memmove(d, s, n);
     return hipSuccess;
@@ -127,9 +131,12 @@ hipError_t launch_eval_stream(const uint8_t* const*, const uint32_t*, uint32_t, 
                               const uint64_t*, const uint32_t*, uint32_t n, uint8_t* tri, int32_t* err, uint64_t* bm,
                               uint32_t stride, uint64_t* rows, uint32_t row_stride, bool keep_rows,
                               uint32_t* stage_ids, uint32_t* slow_count, uint32_t*, hipStream_t, int, bool,
-                              uint32_t) {
-    slow_count[0] = n / 5;
-    slow_count[1] = 0;
+                              uint32_t, bool* zero) {
+    // (as the small-batch instance: the counters left zero, the slow count at [3])
+    slow_count[3] = n / 5;
+    slow_count[0] = slow_count[1] = slow_count[2] = 0;
+    if (zero) *zero = !keep_rows;
+    if (keep_rows) slow_count[0] = n / 5;
     (void)stage_ids;
     if (keep_rows)
         for (uint32_t r = 0; r < n; r++) rows[(size_t)r * row_stride] = r;

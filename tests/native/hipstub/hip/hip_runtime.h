@@ -24,6 +24,7 @@ hipError_t hipMallocRaw(void**, size_t);
 hipError_t hipFree(void*);
 hipError_t hipHostMallocRaw(void**, size_t, unsigned);
 hipError_t hipHostFree(void*);
+hipError_t hipHostGetDevicePointer(void**, void*, unsigned);
 hipError_t hipMemcpy(void*, const void*, size_t, hipMemcpyKind);
 hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t);
 hipError_t hipMemsetAsync(void*, int, size_t, hipStream_t);

@@ -119,3 +119,23 @@ def test_stream_mutated_and_invalid_documents(ctx):
         ctx.set_stream_max(n_max)
         _same(ctx, [(pats, nodes, root)], *_pack(docs))
     ctx.set_stream_max(4096)
+
+
+def test_stream_counters_across_launches(ctx):
+    """The small-batch instance clears its counters for the next launch on the stream (no
+    fill) and publishes the exact-path count apart: repeated batches, and batches of the
+    other kernels in between, all equal to the oracle with the same exact-path count."""
+    from test_stream_scan import INVALID
+
+    rng = np.random.default_rng(93)
+    pats = [("a", 1, "1"), ("b", 2, "v"), ("a.b", 1, "2")]
+    nodes, root = FU.chain(len(pats))
+    docs = list(INVALID) * 2 + [FU.mutate(rng, FU.rand_doc(rng, ws=False)) for _ in range(300)]
+    counts = []
+    for n_max in (4096, 4096, 0, 4096, 4096):  # (stream, stream, lean, stream, stream)
+        ctx.set_stream_max(n_max)
+        _same(ctx, [(pats, nodes, root)], *_pack(docs))
+        counts.append(ctx.last_exact_count())
+    ctx.set_stream_max(4096)
+    stream_counts = [c for c, m in zip(counts, (1, 1, 0, 1, 1)) if m]
+    assert stream_counts[0] > 0 and len(set(stream_counts)) == 1, counts
