@@ -590,15 +590,23 @@ __device__ __forceinline__ void stream_body(const uint8_t* const* __restrict__ s
     if (timing) c1 = __builtin_readcyclecounter();
     const uint64_t *rowp = nullptr, *dwp = nullptr;
     const uint8_t* lds_doc = nullptr;
+    uint64_t ck[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // (timing: the step's and stage B's phase clocks)
     const uint32_t res = stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
-                                                 out_bm, stride, &rowp, &dwp, LAT ? &lds_doc : nullptr);
+                                                 out_bm, stride, &rowp, &dwp, LAT ? &lds_doc : nullptr,
+                                                 timing ? ck : nullptr);
     const uint32_t r = span * per + l;
     if (timing) c2 = __builtin_readcyclecounter();
     auto times = [&](uint32_t rq) {
         if (!timing || l != 0 || !out_bm) return;
         const uint64_t c3 = __builtin_readcyclecounter();
         auto f = [](uint64_t a, uint64_t b) { return ((b - a) >> 4) & 0x1FFFFFull; };
-        out_bm[(size_t)rq * stride] = f(c0, c1) | (f(c1, c2) << 21) | (f(c2, c3) << 42);
+        uint64_t* o = out_bm + (size_t)rq * stride;
+        o[0] = f(c0, c1) | (f(c1, c2) << 21) | (f(c2, c3) << 42);
+        if (stride >= 4 && ck[0] && ck[8]) {  // (the sub-phases: step 0..3, stage B 5..8)
+            o[1] = f(c1, ck[0]) | (f(ck[0], ck[1]) << 21) | (f(ck[1], ck[2]) << 42);
+            o[2] = f(ck[2], ck[3]) | (f(ck[3], c2) << 21) | (f(c2, ck[5]) << 42);
+            o[3] = f(ck[5], ck[6]) | (f(ck[6], ck[7]) << 21) | (f(ck[7], ck[8]) << 42);
+        }
     };
     if constexpr (LAT) {
         // one request per wave: every lane takes part in its stage B (finish_full<true>)
@@ -613,7 +621,7 @@ __device__ __forceinline__ void stream_body(const uint8_t* const* __restrict__ s
             const uint64_t* dw0 = reinterpret_cast<const uint64_t*>(bcast(dwp));
             const uint32_t r0 = span;
             const bool ok = stream::finish_full<true>(r0, blob, d0, lens[r0], RowRef(row0), out_tri, out_err, out_bm,
-                                                      stride, dw0);
+                                                      stride, dw0, timing ? ck : nullptr);
             if (!ok && l == 0) {
                 atomicAdd(slow_count, 1u);
                 stage_ids[atomicAdd(slow_count + 1, 1u)] = r0 | kStageExact;

@@ -63,6 +63,18 @@ constexpr uint32_t kOpenEnd = 1u << 28;
 constexpr uint32_t kTypeUnknown = 7u;
 
 // a span's request: block 0 at arena + base (32-B aligned), its first byte at mis
+// (profiling, kernel mode 53: phase clocks; 0 on the host)
+AJX_HD uint64_t clk_now() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_readcyclecounter();
+#else
+    return 0;
+#endif
+}
+AJX_HD void clk_at(uint64_t* clk, uint32_t k) {
+    if (clk) clk[k] = clk_now();
+}
+
 struct DocEnt {
     uint32_t base_lo, base_hi;
     uint32_t len_mis;  // len | mis << 24
@@ -350,7 +362,7 @@ AJX_HD void fetch(WaveLds& L, const uint8_t* __restrict__ arena, uint32_t t, uin
 // MODE 1 (profiling): the structural pass only (no keys, no captures); 2: no stage B.
 template <int MODE>
 AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t l, const Blk& B, uint64_t H,
-                 Carry& c) {
+                 Carry& c, uint64_t* clk = nullptr) {
     uint8_t* ring = L.ring_raw + 16;
     const uint32_t doc = B.doc;
     const bool head = B.head, live = B.live;
@@ -370,6 +382,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
         rp[0] = V4{B.x[0], B.x[1], B.x[2], B.x[3]};
         rp[1] = V4{B.x[4], B.x[5], B.x[6], B.x[7]};
     }
+    clk_at(clk, 0);  // (the block's loads arrived)
 
     // ---- classification (ajx_lean.h)
     uint32_t d[8];
@@ -498,6 +511,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
     c.depth = (int32_t)wave::readlane((uint32_t)(depth_in + net), 63);
 
     const uint32_t ARR = d[lean::creg(K_SQ)] & (OP | CL);  // [ and ]
+    clk_at(clk, 1);  // (classification, strings, grammar, depth)
 
     // ---- keys (ids) and brackets in document order: the lane's container transform, kind
     // and alternation checks, root close
@@ -657,6 +671,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
     if (req_m && (((stk_in.k >> 16) & req_m) != req_v)) bad |= 1u << req_pos;
     if (bad && live) wave::lds_min(&L.bad[doc], (uint32_t)(pos0 + (int32_t)ctz(bad)));
     bad = 0;
+    clk_at(clk, 2);  // (keys, brackets, the container stack)
 
     if constexpr (MODE != 1) {
         // ---- keys on selector paths: capture their values; elements of captured arrays
@@ -863,6 +878,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
         }
         if (bad && live) wave::lds_min(&L.bad[doc], (uint32_t)(pos0 + (int32_t)ctz(bad)));
     }
+    clk_at(clk, 3);  // (captures, eager patterns)
 }
 
 // Stage B's prelude for a value whose end the stream left open (long values, containers,
@@ -1007,7 +1023,7 @@ AJX_HD bool finish_light(uint32_t r, const uint8_t* blob, const Tabs& T, const u
 template <bool WAVE = false>
 AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint32_t n, RowRef row,
                         uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm,
-                        uint32_t stride, const uint64_t* dwp = nullptr) {
+                        uint32_t stride, const uint64_t* dwp = nullptr, uint64_t* clk = nullptr) {
     const uint32_t lane = WAVE ? wave::lane() : 0u, step = WAVE ? 64u : 1u;
     // (WAVE: a failure in any lane fails the request)
     auto fail_any = [&](bool f) -> bool {
@@ -1034,6 +1050,7 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
         dD = orall(dD);
         dT = orall(dT);
     }
+    clk_at(clk, 5);
     const SelectorPatterns* sps = reinterpret_cast<const SelectorPatterns*>(blob + h->off_sel_patterns);
     bool bad = false;
     for (uint32_t s = lane; s < nr; s += step) {
@@ -1053,6 +1070,7 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
         return false;
     }
     if constexpr (WAVE) wave::sync();
+    clk_at(clk, 6);
     // the selectors the stream does not follow to the end: the exact Get of the rest of the
     // path inside their prefix's value (or on the whole proved document)
     if (sh->n_tails) {
@@ -1098,6 +1116,7 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
         }
         if constexpr (WAVE) wave::sync();
     }
+    clk_at(clk, 7);
     uint64_t t[2], u[2];
     const uint64_t dec[2] = {dD, dT};
     patterns_from_row(blob, d, row, t, u, dec, lane, step);
@@ -1107,6 +1126,7 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
         u[0] = orall(u[0]);
         u[1] = orall(u[1]);
     }
+    clk_at(clk, 8);
     if ((u[0] & ~h->unsupported[0]) | (u[1] & ~h->unsupported[1])) {
         if (lane == 0) row[0] = kRowSlow;
         return false;
@@ -1170,7 +1190,8 @@ AJX_HD uint32_t scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const
                           const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
                           uint32_t span, uint32_t per, uint32_t l, uint8_t* __restrict__ out_tri,
                           int32_t* __restrict__ out_err, uint64_t* __restrict__ out_bm, uint32_t stride,
-                          const uint64_t** row_out, const uint64_t** dw_out, const uint8_t** lds_doc = nullptr) {
+                          const uint64_t** row_out, const uint64_t** dw_out, const uint8_t** lds_doc = nullptr,
+                          uint64_t* clk = nullptr) {
     const Tabs T = tabs_of(blob);
     const uint32_t r = span * per + l;
     const bool my = l < per && r < n;
@@ -1190,7 +1211,7 @@ AJX_HD uint32_t scan_span(WaveLds& L, uint64_t* rows, const uint8_t* blob, const
         Blk nxt{};
         uint64_t Hn = 0;
         if (t + 1u < nsteps) fetch(L, arena, t + 1u, total, l, my_start, my, last_doc, nxt, Hn);
-        step<MODE>(L, rows, T, t, l, cur, Hc, c);
+        step<MODE>(L, rows, T, t, l, cur, Hc, c, t == 0 ? clk : nullptr);
         cur = nxt;
         Hc = Hn;
         last_doc += (uint32_t)__builtin_popcountll(Hn);

@@ -279,9 +279,9 @@ class Context:
         arena = np.frombuffer(b"".join(docs) or b"\0", dtype=np.uint8)
         return self.eval_host_arena(sets, arena, offs, lens, set_of_req, with_bitmap)
 
-    def eval_host_arena(self, sets, arena, offs, lens, set_of_req=None, with_bitmap=True):
+    def eval_host_arena(self, sets, arena, offs, lens, set_of_req=None, with_bitmap=True, bitmap_words=0):
         n = int(lens.shape[0])
-        words = max(1, max((s.n_patterns + 63) // 64 for s in sets))
+        words = max(1, bitmap_words, max((s.n_patterns + 63) // 64 for s in sets))
         nt = sets[0].n_trees
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
