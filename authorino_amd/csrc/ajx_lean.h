@@ -262,10 +262,12 @@ struct Walk {
     uint64_t nlo, nhi;      // trie node per depth 1..16
     uint32_t top, tarr;     // top container's node, is-array
     uint32_t expk;          // top object expects a key (1) or its value (0)
-    uint32_t pnode, pstart; // a key's value pending over a sub-window boundary
-    uint32_t idx, asv0, asv1, nasv;  // element index of the top array; saved indices of outer arrays
-    uint32_t skipd, skipcap, skips;  // squash: depth, captured selector + 1, start (its open)
-    uint32_t cap0, cap0s, cap1, cap1s, ncap;  // open captured containers: sel | depth << 8, start
+    // (the fields the walk touches only at rarer tokens go packed, so the kernel keeps its
+    // state in registers without spilling)
+    uint32_t pend;          // a key's value pending over a sub-window boundary: start | node << 24
+    uint32_t idx, asv, nasv;  // element index of the top array; saved indices of outer arrays (16 bits each)
+    uint32_t skipw, skips;  // squash: depth (bits 0..23) | captured selector + 1 << 24; start (its open)
+    uint32_t caps, cap0s, cap1s, ncap;  // open captured containers: sel | depth << 8 (16 bits each), starts
     uint32_t carry_oq;      // last opening quote before the sub-window being walked
     uint32_t lbs1;          // last backslash before it, + 1 (0 none)
     int32_t root_end;       // position of the root's close
@@ -421,16 +423,14 @@ struct Walk {
         const int32_t s = leaf_sel(node);
         const bool eager = arr && eg && s >= 0 && !ea && (tn[node].flags & 2);  // (its elements compared)
         if (node == kNoNode || (tn[node].n_children == 0 && !eager)) {  // squashed (captured when a leaf)
-            skipd = 1;
-            skipcap = s >= 0 ? (uint32_t)s + 1u : 0u;
+            skipw = 1u | ((s >= 0 ? (uint32_t)s + 1u : 0u) << 24);
             skips = p;
             return;
         }
         if (depth + 1 > kMaxLive) { st = S_SLOW; return; }
         if (tarr) {  // the outer array's element index comes back at its close
-            if (nasv >= 2) { st = S_SLOW; return; }
-            asv1 = nasv == 1 ? idx : asv1;
-            asv0 = nasv == 0 ? idx : asv0;
+            if (nasv >= 2 || idx > 0xFFFFu) { st = S_SLOW; return; }
+            asv = nasv == 1 ? (asv & 0xFFFFu) | (idx << 16) : nasv == 0 ? (asv & 0xFFFF0000u) | idx : asv;
             nasv++;
         }
         depth++;
@@ -448,10 +448,9 @@ struct Walk {
         if (s >= 0) {
             found |= 1ull << s;  // (first match in document order)
             if (ncap >= 2) { st = S_SLOW; return; }
-            const uint32_t v = (uint32_t)s | (depth << 8);
-            cap1 = ncap == 1 ? v : cap1;
+            const uint32_t v = (uint32_t)s | (depth << 8);  // (s < 64, depth <= 16)
+            caps = ncap == 1 ? (caps & 0xFFFFu) | (v << 16) : ncap == 0 ? (caps & 0xFFFF0000u) | v : caps;
             cap1s = ncap == 1 ? p : cap1s;
-            cap0 = ncap == 0 ? v : cap0;
             cap0s = ncap == 0 ? p : cap0s;
             ncap++;
         }
@@ -459,7 +458,7 @@ struct Walk {
     AJX_HD void close(uint32_t p) {
         eager_close();
         if (ncap) {
-            const uint32_t cs = ncap == 2 ? cap1 : cap0, start = ncap == 2 ? cap1s : cap0s;
+            const uint32_t cs = ncap == 2 ? caps >> 16 : caps & 0xFFFFu, start = ncap == 2 ? cap1s : cap0s;
             if ((cs >> 8) == depth) {
                 row[1 + (cs & 0xFFu)] =
                     (uint64_t)start | ((uint64_t)(((p + 1 - start) & 0xFFFFFFu) | ((uint32_t)T_JSON << 24)) << 32);
@@ -476,7 +475,7 @@ struct Walk {
         tarr = (kinds >> depth) & 1u;
         expk = 1;
         if (tarr) {
-            idx = nasv == 2 ? asv1 : asv0;
+            idx = nasv == 2 ? asv >> 16 : asv & 0xFFFFu;
             nasv--;
         }
     }
@@ -524,12 +523,12 @@ struct Walk {
     // walk sub-window c (l: the one after it; its tokens may be taken here: l.tok updated)
     AJX_HD void walk(const Sub& c, Sub& l) {
         uint32_t T;
-        if (skipd) {  // squashing: only brackets (after the squash's own open) matter
+        if (skipw) {  // squashing: only brackets (after the squash's own open) matter
             const int32_t rel = (int32_t)skips - c.base;
             const uint32_t ex = rel < 0 ? ~0u : above((uint32_t)rel);
             const uint32_t o = popc(c.op & ex), x = popc(c.cl & ex);
-            if (x < skipd) {  // the depth can not reach zero here
-                skipd += o - x;
+            if (x < (skipw & 0xFFFFFFu)) {  // the depth can not reach zero here
+                skipw += o - x;
                 T = 0;
             } else {
                 T = (c.op | c.cl) & ex;
@@ -544,11 +543,12 @@ struct Walk {
             const uint32_t i = ctz(T);
             T &= T - 1u;
             const uint32_t p = (uint32_t)(c.base + (int32_t)i);
-            if (skipd) {
+            if (skipw) {
                 if ((c.op >> i) & 1u) {
-                    skipd++;
-                } else if (--skipd == 0) {
-                    if (skipcap) record((int32_t)skipcap - 1, skips, p + 1, T_JSON, 0);
+                    skipw++;
+                } else if (((--skipw) & 0xFFFFFFu) == 0) {
+                    if (skipw >> 24) record((int32_t)(skipw >> 24) - 1, skips, p + 1, T_JSON, 0);
+                    skipw = 0;
                     T = c.tok & above(i);
                 }
                 continue;
@@ -569,8 +569,9 @@ struct Walk {
                 }
                 if (!expk) {  // the pending value string of a key
                     if (kq) { st = S_SLOW; T = 0; break; }
-                    const int32_t s = leaf_sel(pnode);
-                    if (s >= 0) record(s, pstart, p + 1, T_STRING, has_bs(pstart, p, c, l) ? 1u : 0u);
+                    const int32_t s = leaf_sel(pend >> 24);
+                    const uint32_t ps = pend & 0xFFFFFFu;
+                    if (s >= 0) record(s, ps, p + 1, T_STRING, has_bs(ps, p, c, l) ? 1u : 0u);
                     expk = 1;
                     continue;
                 }
@@ -599,14 +600,13 @@ struct Walk {
                         if (s >= 0) record(s, vs, e + 1, T_STRING, has_bs(vs, e, c, l) ? 1u : 0u);
                     } else {
                         expk = 0;
-                        pnode = node;
-                        pstart = vs;
+                        pend = vs | (node << 24);  // (positions < 2^24)
                     }
                 } else if (vb == '{' || vb == '[') {
                     if (rv < 32) T &= ~(1u << rv);
                     else l.tok &= ~(1u << (rv - 32));
                     open(node, vb == '[', vs);
-                    if (skipd) T = rv < 32 ? T & (c.op | c.cl) & above(rv) : 0u;
+                    if (skipw) T = rv < 32 ? T & (c.op | c.cl) & above(rv) : 0u;
                     else T = rv < 32 ? T & above(rv) : 0u;
                 } else if (!scalar(node, vs, vb, c, l, false)) {
                     st = S_SLOW;
@@ -619,13 +619,13 @@ struct Walk {
                 if (depth == 0) {  // the root
                     if (p != 0) { st = S_SLOW; T = 0; break; }
                     open(0, rb(p) == '[', p);
-                    if (skipd) { st = S_SLOW; T = 0; break; }  // (a ruleset whose root node is a leaf)
+                    if (skipw) { st = S_SLOW; T = 0; break; }  // (a ruleset whose root node is a leaf)
                     continue;
                 }
                 if (!tarr) { st = S_SLOW; T = 0; break; }  // (a container where a key belongs)
                 if (ea) eager_elem(false, 0, 0, false);
                 open(elem_node(), rb(p) == '[', p);
-                if (skipd) T &= c.op | c.cl;
+                if (skipw) T &= c.op | c.cl;
                 continue;
             }
             if ((c.cl >> i) & 1u) {
@@ -675,11 +675,10 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     w.top = kNoNode;
     w.tarr = 0;
     w.expk = 1;
-    w.pnode = kNoNode;
-    w.pstart = 0;
-    w.idx = w.asv0 = w.asv1 = w.nasv = 0;
-    w.skipd = w.skipcap = w.skips = 0;
-    w.cap0 = w.cap0s = w.cap1 = w.cap1s = w.ncap = 0;
+    w.pend = (uint32_t)kNoNode << 24;
+    w.idx = w.asv = w.nasv = 0;
+    w.skipw = w.skips = 0;
+    w.caps = w.cap0s = w.cap1s = w.ncap = 0;
     w.carry_oq = 0;
     w.lbs1 = 0;
     w.root_end = 0x7FFFFFFF;
