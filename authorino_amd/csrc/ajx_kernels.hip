@@ -191,11 +191,31 @@ static void launch_slow_list(bool mods, uint32_t sgrid, hipStream_t stream, cons
 // loop waits for each load in turn: a load latency per iteration)
 __device__ __forceinline__ void copy_words(uint4* __restrict__ dst, const uint4* __restrict__ src, uint32_t nq,
                                            uint32_t t, uint32_t nt) {
+    // (the array lives in scratch here, 128 B per lane; the unconditional-load form that
+    // keeps it in registers measured c3 at 3.83 ms against 2.61: the lean kernel's main
+    // loop allocated worse)
     for (uint32_t b = t; b < nq; b += 8u * nt) {
         uint4 v[8];
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++)
             if (b + j * nt < nq) v[j] = src[b + j * nt];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+            if (b + j * nt < nq) dst[b + j * nt] = v[j];
+    }
+}
+
+// copy_words with every load unconditional (past the end, word b again): the array stays
+// in registers (the streaming kernel's per-wave blob copy: c4 serving 7.8 k -> 4.0 k clocks)
+__device__ __forceinline__ void copy_words_reg(uint4* __restrict__ dst, const uint4* __restrict__ src, uint32_t nq,
+                                               uint32_t t, uint32_t nt) {
+    for (uint32_t b = t; b < nq; b += 8u * nt) {
+        uint4 v[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t k = b + j * nt;
+            v[j] = src[k < nq ? k : b];
+        }
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++)
             if (b + j * nt < nq) dst[b + j * nt] = v[j];
@@ -573,7 +593,7 @@ __device__ __forceinline__ void stream_body(const uint8_t* const* __restrict__ s
         uint8_t* wb = reinterpret_cast<uint8_t*>(s_stream_dyn) + w * wave_bytes;
         const uint32_t tb = lean::uni(reinterpret_cast<const RulesetHdr*>(g)->total_bytes);  // (x16)
         if (tb <= wave_off) {
-            copy_words(reinterpret_cast<uint4*>(wb), reinterpret_cast<const uint4*>(g), tb / 16u, l, 64u);
+            copy_words_reg(reinterpret_cast<uint4*>(wb), reinterpret_cast<const uint4*>(g), tb / 16u, l, 64u);
             wave::sync();
             blob = wb;
         } else {
@@ -590,7 +610,11 @@ __device__ __forceinline__ void stream_body(const uint8_t* const* __restrict__ s
     if (timing) c1 = __builtin_readcyclecounter();
     const uint64_t *rowp = nullptr, *dwp = nullptr;
     const uint8_t* lds_doc = nullptr;
-    uint64_t ck[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // (timing: the step's and stage B's phase clocks)
+    uint64_t* ck = L.clk;  // (timing: the step's and stage B's phase clocks)
+    if (timing) {
+        if (l < 9) ck[l] = 0;
+        wave::sync();
+    }
     const uint32_t res = stream::scan_span<MODE>(L, rows, blob, arena, offs, lens, n, span, per, l, out_tri, out_err,
                                                  out_bm, stride, &rowp, &dwp, LAT ? &lds_doc : nullptr,
                                                  timing ? ck : nullptr);
@@ -668,6 +692,34 @@ __device__ __forceinline__ void stream_body(const uint8_t* const* __restrict__ s
     }
 }
 
+// The stage-B list of a small batch, run by the wave that finished last: a call, not
+// inlined, so that the exact scan's registers stay out of the walk's own allocation (the
+// inlined list took the kernel to 256 VGPRs, AGPR spills and ~1,400 SGPR spills)
+template <bool MT>
+__device__ __noinline__ void stream_fin_list(const uint8_t* const* __restrict__ sets,
+                                             const uint32_t* __restrict__ set_of_req,
+                                             const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                                             const uint32_t* __restrict__ lens, uint32_t cnt,
+                                             uint32_t* __restrict__ slow_count, const uint32_t* __restrict__ stage_ids,
+                                             uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
+                                             uint64_t* __restrict__ out_bm, uint32_t stride,
+                                             uint64_t* __restrict__ rows_out, uint32_t row_stride, uint32_t l) {
+    for (uint32_t i = l; i < cnt; i += 64u) {
+        const uint32_t e = stage_ids[i];
+        const uint32_t r = e & ~kStageExact;
+        const uint8_t* blob = sets[MT ? set_of_req[r] : 0];
+        bool ok = false;
+        if (!(e & kStageExact)) {
+            ok = stream::finish_full(r, blob, arena + offs[r], lens[r], wave_row(rows_out, row_stride, r), out_tri,
+                                     out_err, out_bm, stride);
+            if (!ok) atomicAdd(slow_count, 1u);
+        }
+        if (!ok)
+            eval_scan_one<false>(r, sets, MT ? set_of_req : nullptr, arena, offs, lens, out_tri, out_err, out_bm,
+                                 stride, nullptr);
+    }
+}
+
 // The kernel: the span's walk (stream_body), then, with FIN (a small batch without
 // modifier chains), the stage-B list in the wave that finishes last: the requests left to
 // the exact scan and those whose stage B could not run on the LDS copy — no second launch.
@@ -696,20 +748,9 @@ __global__ __launch_bounds__(256) void ajx_scan_stream(const uint8_t* const* __r
         if (!wave::readlane(last, 0)) return;
         __threadfence();
         const uint32_t cnt = __hip_atomic_load(slow_count + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t i = l; i < cnt; i += 64u) {
-            const uint32_t e = stage_ids[i];
-            const uint32_t r = e & ~kStageExact;
-            const uint8_t* blob = sets[MT ? set_of_req[r] : 0];
-            bool ok = false;
-            if (!(e & kStageExact)) {
-                ok = stream::finish_full(r, blob, arena + offs[r], lens[r], wave_row(rows_out, row_stride, r), out_tri,
-                                         out_err, out_bm, stride);
-                if (!ok) atomicAdd(slow_count, 1u);
-            }
-            if (!ok)
-                eval_scan_one<false>(r, sets, MT ? set_of_req : nullptr, arena, offs, lens, out_tri, out_err, out_bm,
-                                     stride, nullptr);
-        }
+        if (cnt)
+            stream_fin_list<MT>(sets, set_of_req, arena, offs, lens, cnt, slow_count, stage_ids, out_tri, out_err,
+                                out_bm, stride, rows_out, row_stride, l);
         // every other wave is done with the counters: back to zero for the next launch on
         // this stream (no fill before it), the slow count kept at [3] for the host
         __threadfence();

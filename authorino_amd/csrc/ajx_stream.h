@@ -112,6 +112,7 @@ struct WaveLds {
     uint32_t bad[kSpan];       // first position failing a check (min)
     uint32_t root_end[kSpan];  // position of the root's close (min)
     uint64_t heads[2];         // a step's lanes holding a document's first block (by parity)
+    uint64_t clk[9];           // (profiling, kernel mode 53: phase clocks; LDS, not scratch)
 };
 #if defined(__HIPCC__)
 __host__ __device__

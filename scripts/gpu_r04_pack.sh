@@ -1,5 +1,5 @@
 # round 4: the lean walker with its rare fields packed (spills): parity, c2 / c3 times, scratch
-R=$GRAFT_REPO_ROOT; cd $R && O=gpurun_out/${OUT:-r04pack} && mkdir -p $O && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT; cd $R && O=gpurun_out/${OUT:-r04pack}/pack && mkdir -p $O && export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_stream.py -x -q --timeout 150 --timeout-method thread > $O/pytest.log 2>&1 || { tail -20 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 for wl in c2 c3; do

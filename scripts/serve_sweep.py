@@ -16,7 +16,7 @@ def main():
     w = workloads.make("c4", n=n)
     rss = [ctx.compile_expression(e) for e in w.sets]
     tri, _, _ = ctx.eval_host_arena(rss, w.arena, w.offs, w.lens, set_of_req=w.set_of_req)
-    for workers in (2, 3, 4):
+    for workers in [int(x) for x in os.environ.get("SWEEP_WORKERS", "2,3,4").split(",")]:
         for threads, window_us in ((64, 50), (64, 20), (256, 200)):
             b = runtime.Batcher(ctx, max_batch=8192, window_us=window_us, workers=workers)
             try:
