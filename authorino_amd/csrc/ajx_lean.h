@@ -267,8 +267,7 @@ struct Walk {
     uint32_t pend;          // a key's value pending over a sub-window boundary: start | node << 24
     uint32_t idx, asv, nasv;  // element index of the top array; saved indices of outer arrays (16 bits each)
     uint32_t skipw, skips;  // squash: depth (bits 0..23) | captured selector + 1 << 24; start (its open)
-    uint32_t caps, ncap;    // open captured containers: sel | depth << 8 (16 bits each; their starts
-                            // wait in their rows' records)
+    uint32_t caps, cap0s, cap1s, ncap;  // open captured containers: sel | depth << 8 (16 bits each), starts
     uint32_t carry_oq;      // last opening quote before the sub-window being walked
     uint32_t lbs1;          // last backslash before it, + 1 (0 none)
     uint64_t found;
@@ -450,16 +449,16 @@ struct Walk {
             if (ncap >= 2) { st = S_SLOW; return; }
             const uint32_t v = (uint32_t)s | (depth << 8);  // (s < 64, depth <= 16)
             caps = ncap == 1 ? (caps & 0xFFFFu) | (v << 16) : ncap == 0 ? (caps & 0xFFFF0000u) | v : caps;
-            row[1 + (uint32_t)s] = (uint64_t)p;  // (the start; the record is completed at the close)
+            cap1s = ncap == 1 ? p : cap1s;
+            cap0s = ncap == 0 ? p : cap0s;
             ncap++;
         }
     }
     AJX_HD void close(uint32_t p) {
         eager_close();
         if (ncap) {
-            const uint32_t cs = ncap == 2 ? caps >> 16 : caps & 0xFFFFu;
+            const uint32_t cs = ncap == 2 ? caps >> 16 : caps & 0xFFFFu, start = ncap == 2 ? cap1s : cap0s;
             if ((cs >> 8) == depth) {
-                const uint32_t start = (uint32_t)row[1 + (cs & 0xFFu)];
                 row[1 + (cs & 0xFFu)] =
                     (uint64_t)start | ((uint64_t)(((p + 1 - start) & 0xFFFFFFu) | ((uint32_t)T_JSON << 24)) << 32);
                 ncap--;
@@ -678,7 +677,7 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     w.pend = (uint32_t)kNoNode << 24;
     w.idx = w.asv = w.nasv = 0;
     w.skipw = w.skips = 0;
-    w.caps = w.ncap = 0;
+    w.caps = w.cap0s = w.cap1s = w.ncap = 0;
     w.carry_oq = 0;
     w.lbs1 = 0;
     w.found = 0;

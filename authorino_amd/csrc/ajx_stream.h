@@ -1145,6 +1145,33 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
     // (64 per coalesced read) instead of one dependent memory read each
     auto fold = [&](const uint32_t* c, uint32_t nc, int32_t* ep) -> uint8_t {
         if constexpr (WAVE) {
+            // a flat All / Any (open, patterns, close; up to 64 words): the lanes hold one
+            // word each and the result is the first leaf, in code order, that is not the
+            // group's identity (the interpreter's sticky value), else the identity
+            if (nc >= 3 && nc <= 64) {
+                const uint32_t cw = lane < nc ? c[lane] : 0u;
+                const uint32_t op0 = wave::readlane(cw, 0) >> 24, opl = wave::readlane(cw, nc - 1u) >> 24;
+                const bool leaf = lane >= 1 && lane + 1u < nc;
+                const uint64_t leaves = wave::ballot(leaf), pats = wave::ballot(leaf && (cw >> 24) == C_PAT);
+                if ((op0 == C_OPEN_AND || op0 == C_OPEN_OR) && opl == C_CLOSE && pats == leaves) {
+                    const uint32_t arg = cw & 0xFFFFFFu, q = arg >> 6;
+                    const uint64_t bit = 1ull << (arg & 63u);
+                    const uint32_t v = ((q ? se[1] : se[0]) & bit)  ? (uint32_t)V_E
+                                       : ((q ? u[1] : u[0]) & bit) ? (uint32_t)V_U
+                                       : ((q ? t[1] : t[0]) & bit) ? (uint32_t)V_T
+                                                                    : (uint32_t)V_F;
+                    const uint32_t ident = op0 == C_OPEN_OR ? (uint32_t)V_F : (uint32_t)V_T;
+                    const uint64_t stick = wave::ballot(leaf && v != ident);
+                    if (!stick) {
+                        *ep = -1;
+                        return (uint8_t)ident;
+                    }
+                    const uint32_t k = (uint32_t)__builtin_ctzll(stick);
+                    const uint32_t vk = wave::readlane(v, k), ak = wave::readlane(arg, k);
+                    *ep = (vk == V_E || vk == V_U) ? (int32_t)ak : -1;
+                    return (uint8_t)vk;
+                }
+            }
             uint32_t creg = 0, cbase = 0xFFFFFFFFu;
             return run_fold_bits_f(
                 [&](uint32_t k) -> uint32_t {
