@@ -564,7 +564,8 @@ static int eval_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint3
                (reinterpret_cast<const ajx::RulesetHdr*>(sets[i]->c.blob.data())->flags & ajx::kFlagBufs) != 0;
     // capture rows kept for authjx_select_from_eval_device: one forest ruleset
     // (authjx_compile_forest), a full kernel
-    const bool full = ablate == 0 || ablate == 41 || ablate == 52 || (ablate >= 10 && ablate <= 12);
+    const bool full = ablate == 0 || ablate == 41 || ablate == 52 || (ablate >= 10 && ablate <= 12) ||
+                      (ablate >= 15 && ablate <= 18);  // (15..18: lean ablations, length order kept)
     const auto* h0 = reinterpret_cast<const ajx::RulesetHdr*>(sets[0]->c.blob.data());
     const bool keep_rows = !force_scan && n_sets == 1 && full && h0->pad1[0] != 0;
     w->rows_rs = keep_rows ? sets[0] : nullptr;
@@ -607,7 +608,7 @@ static int eval_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint3
         HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                      d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
                                      w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
-                                     ablate < 20 ? ablate : 0, perm, mods));
+                                     ablate < 20 ? ablate : 0, perm, mods, keep_rows));
     }
     return batch_done(w, sets, n_sets);
 }

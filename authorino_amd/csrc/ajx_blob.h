@@ -226,7 +226,10 @@ constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the
 // Patterns the lean scan decides while it captures (ajx_lean.h): per selector, its first
 // two patterns (index < 64) that compare an unescaped string value's text with a literal
 // of at most 16 bytes (eq, neq, incl / excl on the value alone), and incl / excl over
-// an array of unescaped strings. m: pattern | op << 8 | literal length << 16 | 1 << 31.
+// an array of unescaped strings; a literal value (true / false / null) decides them by the
+// literal's litf. m: pattern | op << 8 | literal length << 16 | litf << 24 | 1 << 31.
+// pad[0] bit 0 (kEagerAll): those are every pattern of the selector (a decided value needs
+// no capture record for stage B).
 struct EagerSel {
     uint32_t lit[2][4];
     uint32_t m[2];
@@ -234,6 +237,7 @@ struct EagerSel {
 };
 static_assert(sizeof(EagerSel) == 48, "EagerSel layout");
 constexpr uint32_t kEagerValid = 1u << 31;  // EagerSel::m[k] holds an eager pattern
+constexpr uint32_t kEagerAll = 1u;           // EagerSel::pad[0]
 
 // ---- streaming scan (ajx_stream.h) ------------------------------------------------
 // The stream resolves object keys without their parent: every distinct object key of the

@@ -793,17 +793,22 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             bool any = false;
             for (size_t sidx = 0; sidx < sels.size(); sidx++) {
                 uint32_t k = 0;
-                bool arr_ops = false;
+                bool arr_ops = false, all = true;
                 for (uint16_t pi : sel_pats[sidx]) {
                     const Pattern& pt = pats[pi];
-                    if (k >= 2 || pi >= 64 || pt.state != P_OK || pt.lit_len > 16) continue;
-                    if (pt.op != OP_EQ && pt.op != OP_NEQ && pt.op != OP_INCL && pt.op != OP_EXCL) continue;
+                    if (k >= 2 || pi >= 64 || pt.state != P_OK || pt.lit_len > 16 ||
+                        (pt.op != OP_EQ && pt.op != OP_NEQ && pt.op != OP_INCL && pt.op != OP_EXCL)) {
+                        all = false;
+                        continue;
+                    }
                     if (pt.lit_len) std::memcpy(eg[sidx].lit[k], lits.data() + pt.lit_off, pt.lit_len);
-                    eg[sidx].m[k] = (uint32_t)pi | ((uint32_t)pt.op << 8) | (pt.lit_len << 16) | kEagerValid;
+                    eg[sidx].m[k] = (uint32_t)pi | ((uint32_t)pt.op << 8) | (pt.lit_len << 16) |
+                                    ((uint32_t)(pt.litf & 7u) << 24) | kEagerValid;
                     arr_ops = arr_ops || pt.op == OP_INCL || pt.op == OP_EXCL;
                     k++;
                     any = true;
                 }
+                if (all && k) eg[sidx].pad[0] = kEagerAll;
                 if (arr_ops)
                     for (size_t i = 0; i < trie.size(); i++)
                         if (trie[i].selector == (int16_t)sidx) tn[i].flags |= 2;

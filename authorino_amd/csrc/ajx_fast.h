@@ -367,46 +367,18 @@ struct Scan {
     // closing quote of a key at block offset i (doc position p)
     AJX_HD void key_closed(uint32_t p, uint32_t i) {
         pending = kNoNode;
-#ifdef AJX_ABLATE_FAST_NOKEYS
-        return;  // profiling: no selector ever matches (the grammar walk alone)
-#endif
         const uint32_t parent = top_node;
         if (parent == kNoNode) return;
         // (a live node always has children: open_container stores only those)
         str_open = open_before(i);
-#ifndef AJX_ABLATE_KEY_NOESC  // (profiling variants of the key lookup; outputs may differ)
         const uint32_t lb = last_bs_before(i);
         if (lb != ~0u && lb > str_open) { st = X_SLOW; return; }  // escaped key on a live path
-#endif
         const uint32_t k0 = str_open + 1, klen = p - k0;
-#ifdef AJX_ABLATE_KEY_NOSIG
-        uint64_t sig = klen;
-#else
         uint64_t sig = tail8(i);
         if (klen < 8) sig = klen ? sig >> (8 * (8 - klen)) : 0ull;
-#endif
         if (klen >= kIndexKeyLen) return;
         const uint32_t log2 = ks_meta & 0xFFu, want = klen | (parent << 16), mask = (1u << log2) - 1u;
         const uint32_t at = key_slot_hash(sig, klen, parent, log2, ks_mult);
-#ifdef AJX_KEY_UNROLL  // (experiment: the key_probes <= 4 slots read at once, no loop)
-        if ((ks_meta >> 8) <= kKeyProbes) {
-            uint32_t cand = 0, node = kNoNode, koff = 0;
-#pragma unroll
-            for (int q = (int)kKeyProbes - 1; q >= 0; q--) {
-                const KeySlot sl = ks[(at + (uint32_t)q) & mask];
-                const bool c = (uint32_t)q < (ks_meta >> 8) && sl.meta != kEmptySlot && sl.sig == sig &&
-                               (sl.meta & 0xFFFFFFu) == want;
-                cand += c ? 1u : 0u;
-                node = c ? sl.meta >> 24 : node;
-                koff = c ? sl.key_off : koff;
-            }
-            if (cand == 1) {
-                if (klen <= 8 || key_rest_equal(k0, klen, koff)) pending = node;
-                return;
-            }
-            if (cand == 0) return;
-        }
-#endif
         // every key of the table sits within key_probes slots of its home (the compiler grows
         // the table for that), so the probe sequence is bounded by it, not by an empty slot
         uint32_t pos = at;
@@ -415,18 +387,12 @@ struct Scan {
             if (slot.meta == kEmptySlot) return;
             if (slot.sig != sig || (slot.meta & 0xFFFFFFu) != want) continue;
             if (klen <= 8 || key_rest_equal(k0, klen, slot.key_off)) { pending = slot.meta >> 24; return; }
-#ifdef AJX_ABLATE_KEY_PROBE1
-            return;
-#endif
         }
     }
     // the bytes of a key [k0, k0 + klen) before its last 8 equal the literal at key_off
     AJX_HD bool key_rest_equal(uint32_t k0, uint32_t klen, uint32_t key_off) const {
         const uint8_t* kl = lits + key_off;
         const uint32_t a0 = k0 + (wa - (uint32_t)bpos);  // ring position of the key's first byte
-#ifdef AJX_ABLATE_KEY_NOCMP
-        return true;
-#endif
         if (a0 + 64u >= wa) {  // the key began in the ring's windows: compare from LDS
             for (uint32_t k = 0; k + 8 < klen; k += 4) {
                 const uint32_t r = klen - 8 - k;
@@ -458,12 +424,7 @@ struct Scan {
     AJX_HD void token(uint32_t c, uint32_t i) {
         const uint32_t p = (uint32_t)(bpos + (int32_t)i);
         if (gap_cnt) {
-#ifdef AJX_ABLATE_FAST_NOSCALAR
-            st = X_COMMA_OR_CLOSE;
-            if (false) {  // profiling: scalars not validated / recorded
-#else
             if ((st != X_VALUE && st != X_VALUE_OR_CLOSE) || !scalar_value() || (c != ',' && c != ']' && c != '}')) {
-#endif
                 st = X_SLOW;
                 return;
             }
@@ -582,19 +543,6 @@ struct Scan {
             gap_cnt += popc64f(toks) + popc64f(ns);
             return;
         }
-#ifdef AJX_ABLATE_FAST_WALK
-        {  // profiling: iterate the tokens and read each byte, nothing else
-            uint32_t acc = 0;
-            while (toks) {
-                const uint32_t i = ctz64f(toks);
-                toks &= toks - 1;
-                acc += byte_at(i);
-            }
-            gap_cnt += acc & 1u;
-            if (bp + 64 >= (int32_t)n) st = X_DONE;
-            return;
-        }
-#endif
         uint64_t below = 0;  // bits already consumed
         while (toks) {
             const uint32_t i = ctz64f(toks);

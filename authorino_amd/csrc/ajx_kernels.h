@@ -50,7 +50,8 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false);
+                            int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false,
+                            bool keep_rows = true);
 
 // The streaming kernel (ajx_stream.h), its stage B (ajx_stream_finish) and the exact scan of
 // what they hand over: one ruleset for the batch (sets[0], staged in LDS); stream_eligible

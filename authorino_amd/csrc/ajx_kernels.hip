@@ -187,21 +187,28 @@ static void launch_slow_list(bool mods, uint32_t sgrid, hipStream_t stream, cons
 // patterns, literals, DFA tables, fold code — h->total_bytes, a multiple of 16) is
 // copied into dynamic LDS once per workgroup; every thread reaches the barrier. All
 // table reads of the scan and the patterns are then ds_reads.
-// copies nq 16-byte words, eight loads in flight per thread before their stores (a plain
-// loop waits for each load in turn: a load latency per iteration)
+// copies nq 16-byte words, four loads in flight per thread before their stores. The source
+// is read as global memory (a blob pointer loaded from the set table is generic: flat
+// loads otherwise), every load unconditional (a clamped index past the end), so that
+// nothing goes to scratch.
 __device__ __forceinline__ void copy_words(uint4* __restrict__ dst, const uint4* __restrict__ src, uint32_t nq,
                                            uint32_t t, uint32_t nt) {
-    // (the array lives in scratch here, 128 B per lane; the unconditional-load form that
-    // keeps it in registers measured c3 at 3.83 ms against 2.61: the lean kernel's main
-    // loop allocated worse)
-    for (uint32_t b = t; b < nq; b += 8u * nt) {
-        uint4 v[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++)
-            if (b + j * nt < nq) v[j] = src[b + j * nt];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++)
-            if (b + j * nt < nq) dst[b + j * nt] = v[j];
+#if defined(__HIP_DEVICE_COMPILE__)
+    const __attribute__((address_space(1))) uint4* g = (const __attribute__((address_space(1))) uint4*)src;
+#else
+    const uint4* g = src;  // (host pass of the kernel source: never run)
+#endif
+    const uint32_t last = nq - 1u;
+    for (uint32_t b = t; b < nq; b += 4u * nt) {
+        const uint32_t k1 = b + nt, k2 = b + 2u * nt, k3 = b + 3u * nt;
+        const uint4 v0 = g[b];
+        const uint4 v1 = g[k1 < nq ? k1 : last];
+        const uint4 v2 = g[k2 < nq ? k2 : last];
+        const uint4 v3 = g[k3 < nq ? k3 : last];
+        dst[b] = v0;
+        if (k1 < nq) dst[k1] = v1;
+        if (k2 < nq) dst[k2] = v2;
+        if (k3 < nq) dst[k3] = v3;
     }
 }
 
@@ -412,13 +419,15 @@ constexpr uint32_t kLeanRingBytesPerWave = 64 * lean::kRingStride;
 #ifndef AJX_LEAN_MAXBLOCK
 #define AJX_LEAN_MAXBLOCK kFastMaxBlock
 #endif
-template <bool SHARED>
+// ABL: profiling ablations (kernel modes 15..18, lean::scan_doc): stage A cut short, no stage B
+template <bool SHARED, int ABL = 0>
 __global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_lean(
     const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
     uint64_t* __restrict__ rows, uint32_t row_stride, uint32_t* __restrict__ slow_count,
     uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-    uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t ring_off, const uint32_t* __restrict__ perm) {
+    uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t ring_off, const uint32_t* __restrict__ perm,
+    uint32_t keep_rows) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t r = k < n ? (perm ? perm[k] : k) : 0u;
     const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : set_of_req[r]]);
@@ -440,9 +449,14 @@ __global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_le
             }
             return Block16{0u, 0u, 0u, 0u};
         };
-        ok = lean::scan_doc(blob, blob_tables(blob), d, len, row, ring, threadIdx.x & 63u, load, dec);
+        ok = lean::scan_doc<ABL>(blob, blob_tables(blob), d, len, row, ring, threadIdx.x & 63u, load, dec,
+                                 keep_rows);
     } else {
         row[0] = kRowSlow;
+    }
+    if constexpr (ABL != 0) {
+        if (dec[0] ^ dec[1]) row[0] ^= dec[0] ^ dec[1];
+        return;
     }
     if (!ok) {
         slow_ids[atomicAdd(slow_count, 1u)] = r;
@@ -821,6 +835,9 @@ static_assert(kStreamSpan == stream::kSpan, "requests per wave");
 
 // 4-wave workgroups (the kernel's launch bounds), each with its own blob copy
 constexpr uint32_t kStreamBlock = 256;
+// the largest batch whose stage-B list the last wave runs itself (FIN): at most 8 list
+// entries per lane
+constexpr uint32_t kFinMaxN = 512;
 
 hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, uint32_t blob_bytes,
                               uint32_t n_rec, const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
@@ -898,7 +915,12 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
                        d_slow_count, d_slow_ids, d_stage_ids, d_tri, d_err, d_bm, stride, wave_off, wave_bytes,       \
                        d_rows, row_stride, (keep_rows ? 1u : 0u) | (timing ? 2u : 0u), per, merge ? 1u : 0u)
     const bool lat = merge && !keep_rows;
-    const bool fin = lat && !mods;  // (stage B and the exact scan in the last wave: no second launch)
+    // (stage B and the exact scan in the last wave: no second launch). Only for batches of at
+    // most kFinMaxN requests: that wave walks the list 64 entries at a time, so a large batch
+    // of requests the stream cannot finish (long or deeply nested documents) would put
+    // thousands of exact scans behind one wave; larger batches take the grid-stride
+    // ajx_stream_finish launch
+    const bool fin = lat && !mods && n <= kFinMaxN;
     if (mt && fin)
         AJX_STREAM_LAUNCH(0, true, true, true);
     else if (mt && lat)
@@ -1204,7 +1226,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode, const uint32_t* d_perm, bool mods) {
+                            int mode, const uint32_t* d_perm, bool mods, bool keep_rows) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
     // workgroup size by the waves a CU holds (each workgroup stages its own blob copy)
@@ -1229,7 +1251,11 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             reinterpret_cast<const void*>(&ajx_scan_fast<2, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fused),
                             reinterpret_cast<const void*>(&ajx_scan_lean<true>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<false>)};
+                            reinterpret_cast<const void*>(&ajx_scan_lean<false>),
+                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 1>),
+                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 2>),
+                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 3>),
+                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 4>)};
         for (const void* k : ks) {
             const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             if (r != hipSuccess) return r;
@@ -1268,6 +1294,16 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
             hipLaunchKernelGGL((ajx_patterns<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
         }
+    } else if (mode >= 15 && mode <= 18) {  // profiling: lean stage-A ablations (one staged ruleset)
+        if (!shared) return hipErrorInvalidValue;
+        const uint32_t lblock = lean_block(shared_blob_bytes), lgrid = (n + lblock - 1) / lblock;
+        const uint32_t llds = ring_off + (lblock / 64) * kLeanRingBytesPerWave;
+        auto k = mode == 15 ? &ajx_scan_lean<true, 1> : mode == 16 ? &ajx_scan_lean<true, 2>
+               : mode == 17 ? &ajx_scan_lean<true, 3> : &ajx_scan_lean<true, 4>;
+        hipLaunchKernelGGL(k, dim3(lgrid), dim3(lblock), llds, stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, n,
+                           d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, ring_off, d_perm,
+                           keep_rows ? 1u : 0u);
+        return hipGetLastError();
     } else if (!d_set_of_req) {  // the lean single-pass kernel (one ruleset)
         // (multi-tenant batches: the staged tenant scanner below. Measured on c4, the lean
         // scan with per-lane table parameters took 6.39 ms and one pass per ruleset of a
@@ -1278,11 +1314,11 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
         if (shared)
             hipLaunchKernelGGL((ajx_scan_lean<true>), dim3(lgrid), dim3(lblock), llds, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
-                               d_bm, stride, ring_off, d_perm);
+                               d_bm, stride, ring_off, d_perm, keep_rows ? 1u : 0u);
         else
             hipLaunchKernelGGL((ajx_scan_lean<false>), dim3(lgrid), dim3(lblock), llds, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
-                               d_bm, stride, ring_off, d_perm);
+                               d_bm, stride, ring_off, d_perm, keep_rows ? 1u : 0u);
     } else if (shared_blob_bytes) {
         // multi-tenant batch (shared_blob_bytes != 0: staging on): each workgroup stages its
         // runs' rulesets, those that fit (ajx_scan_fused_tenant);

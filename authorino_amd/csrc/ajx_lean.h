@@ -217,11 +217,6 @@ AJX_HD uint32_t uni(uint32_t x) {
     return x;
 #endif
 }
-template <class P>
-AJX_HD P* unip(P* p) {
-    const uint64_t v = (uint64_t)(uintptr_t)p;
-    return (P*)(uintptr_t)((uint64_t)uni((uint32_t)v) | ((uint64_t)uni((uint32_t)(v >> 32)) << 32));
-}
 
 // gjson's value-start bytes (parseObject / parseArray): " { [ n t f + - 0-9 i I N
 AJX_HD bool scalar_start(uint32_t b) {
@@ -231,15 +226,24 @@ AJX_HD bool scalar_start(uint32_t b) {
 
 #if !defined(__HIP_DEVICE_COMPILE__) && defined(AJX_LEAN_COUNT)
 inline uint64_t g_lean_iters = 0, g_lean_subs = 0;  // (host test builds: walker iterations, sub-windows)
+inline uint32_t* g_lean_trace = nullptr;  // (host test builds: sub-window << 8 | token kind per iteration)
+inline uint32_t g_lean_trace_n = 0, g_lean_trace_cap = 0;
 #define AJX_LEAN_TICK(x) (x)++
+#define AJX_LEAN_TRACE(k) \
+    (g_lean_trace && g_lean_trace_n < g_lean_trace_cap ? (void)(g_lean_trace[g_lean_trace_n++] = (uint32_t)(g_lean_subs << 8 | (k))) : (void)0)
 #else
 #define AJX_LEAN_TICK(x) ((void)0)
+#define AJX_LEAN_TRACE(k) ((void)0)
 #endif
+// (token kinds of the trace: 0 squashed, 1 string element, 2 a key's string value from an
+// earlier sub-window, 3 key + string, 4 key + container, 5 key + scalar, 6 root, 7 element
+// container, 8 close, 9 scalar element)
 // per lane: 4 slots of 32 B. 16-byte chunk k of a lane's ring sits at chunk k ^ (lane & 7)
 // (ring_off), so that the 8 lanes of a ds_write_b128 lane group hit all 32 banks
 constexpr uint32_t kRingStride = 128;
 constexpr uint32_t kMaxLive = 16;      // containers on selector paths nested (deeper: exact scan)
 constexpr uint32_t kIdxKeyLen = kIndexKeyLen;
+constexpr uint32_t kRingKeyLen = 31;  // keys the walk compares from the ring (see Walk::lookup)
 
 enum : uint32_t { S_RUN = 0, S_DONE = 1, S_SLOW = 2 };
 
@@ -276,6 +280,7 @@ struct Walk {
     const EagerSel* eg;
     uint64_t eT, eD;
     uint32_t ea;
+    uint32_t keep;  // every capture record goes to the row (a caller reads the rows)
 
     AJX_HD uint32_t ro(uint32_t a) const { return ((a & 0x70u) ^ sw16) | (a & 15u); }  // ring offset a (0..127)
     AJX_HD uint32_t rw(uint32_t q) const { return *reinterpret_cast<const uint32_t*>(ring + ro(q & 127u)); }
@@ -311,13 +316,17 @@ struct Walk {
         if (s < 0 || ((found >> s) & 1)) return -1;
         return s;
     }
+    // a captured value of selector s: doc [start, end), gjson type, has escapes. The
+    // selector's eager patterns (EagerSel) are decided on an unescaped string's contents or
+    // a literal's String() ("true", "false", ""); the capture record goes to the row unless
+    // they were every pattern of the selector (and the caller keeps no rows)
     AJX_HD void record(int32_t s, uint32_t start, uint32_t end, uint32_t type, uint32_t esc) {
         found |= 1ull << s;
-        row[1 + (uint32_t)s] =
-            (uint64_t)start | ((uint64_t)(((end - start) & 0xFFFFFFu) | (type << 24) | (esc << 27)) << 32);
-        if (eg && type == T_STRING && !esc) {  // the selector's eager patterns on the value alone
+        bool dec = false;
+        const bool lit = type == T_TRUE || type == T_FALSE || type == T_NULL;
+        if (eg && ((type == T_STRING && !esc) || lit)) {
             const EagerSel e = eg[s];
-            const uint32_t mt = eager_match(e, start + 1u, end - start - 2u);
+            const uint32_t mt = lit ? lit_match(e, type) : eager_match(e, start + 1u, end - start - 2u);
 #pragma unroll
             for (int k = 0; k < 2; k++) {
                 const uint32_t m = e.m[k], op = (m >> 8) & 0xFFu;
@@ -326,7 +335,25 @@ struct Walk {
                 eD = (m & kEagerValid) ? eD | bit : eD;
                 eT = (m & kEagerValid) && yes ? eT | bit : eT;
             }
+            dec = (e.pad[0] & kEagerAll) != 0;
         }
+        if (!dec || keep)
+            row[1 + (uint32_t)s] =
+                (uint64_t)start | ((uint64_t)(((end - start) & 0xFFFFFFu) | (type << 24) | (esc << 27)) << 32);
+    }
+    // bit k: entry k's literal equals a literal value's String() (EagerSel litf bits); null's
+    // Value.Array() is empty, so incl / excl never find it
+    AJX_HD static uint32_t lit_match(const EagerSel& e, uint32_t type) {
+        const uint32_t litb = type == T_TRUE ? (uint32_t)kLitTrue : type == T_FALSE ? (uint32_t)kLitFalse
+                                                                                    : (uint32_t)kLitEmpty;
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t m = e.m[k], op = (m >> 8) & 0xFFu;
+            const bool arr = op == OP_INCL || op == OP_EXCL;
+            r |= ((m >> 24) & litb) && !(type == T_NULL && arr) ? 1u << k : 0u;
+        }
+        return r;
     }
     // bit k: entry k's literal equals the string content [a, a + cl) (ring bytes; cl <= 16
     // for a match, and then the content lies in the ring's window)
@@ -377,33 +404,36 @@ struct Walk {
     // the key table: (sig, len, parent) -> child node (kNoNode none). len = kIdxKeyLen:
     // sig is an array index. A hit on a key longer than 8 bytes also compares its head
     // (bytes [ks, len - 8) of the key, starting at doc position ks).
+    // Keys of up to kRingKeyLen bytes are read from the ring: the walk looks a key up in the
+    // sub-window holding its closing quote, and the ring still holds the 32 bytes before
+    // that sub-window (64 for the window's first one). Longer keys read the document (a
+    // global load, which also waits for the next window's loads in flight: rare).
     AJX_HD uint32_t lookup(uint64_t sig, uint32_t len, uint32_t parent, uint32_t kstart) const {
         const uint32_t want = len | (parent << 16);
         uint32_t h = (uint32_t)sig ^ (((uint32_t)(sig >> 32) << 13) | ((uint32_t)(sig >> 32) >> 19)) ^ (len << 24) ^
                      (parent << 16);
         h = (h * ks_mult) >> ks_shift;
-        // a longer key's head (bytes [kstart, kstart + len - 8)): its first 8 bytes from the ring
         const bool longk = len > 8 && len != kIdxKeyLen;
-        const uint64_t hm = (len - 8) >= 8 ? ~0ull : ((1ull << (8 * ((len - 8) & 7))) - 1ull);
-        // (keys of 9..16 bytes start in the ring's window; longer ones are read from the document)
-        const uint64_t head =
-            !longk ? 0ull
-                   : (len <= 16 ? r64((kstart + mis) & 127u)
-                                : (uint64_t)load_u32_any(d + kstart) | ((uint64_t)load_u32_any(d + kstart + 4) << 32)) &
-                         hm;
         uint32_t node = kNoNode;
         for (uint32_t t = 0; t < ks_probes; t++) {
             const KeySlot sl = ks[(h + t) & ks_mask];
             bool hit = sl.meta != kEmptySlot && sl.sig == sig && (sl.meta & 0xFFFFFFu) == want;
             // (keys sharing their last 8 bytes, length and parent sit in later slots)
-            if (hit && longk) {
-                const uint8_t* kl = lits + sl.key_off;
-                const uint64_t b = (uint64_t)load_u32_any(kl) | ((uint64_t)load_u32_any(kl + 4) << 32);
-                hit = ((head ^ b) & hm) == 0 && (len <= 16 || key_rest_equal(kstart + 8, len - 16, kl + 8));
-            }
+            if (hit && longk) hit = key_head_equal(kstart, len - 8, lits + sl.key_off);
             node = hit ? sl.meta >> 24 : node;
         }
         return node;
+    }
+    // the key's bytes [k0, k0 + cnt) equal kl[0, cnt), 8 at a time (ring) or byte by byte
+    AJX_HD bool key_head_equal(uint32_t k0, uint32_t cnt, const uint8_t* kl) const {
+        if (cnt + 8 > kRingKeyLen) return key_rest_equal(k0, cnt, kl);
+        for (uint32_t k = 0; k < cnt; k += 8) {
+            const uint32_t r = cnt - k;
+            const uint64_t m = r >= 8 ? ~0ull : ((1ull << (8 * r)) - 1ull);
+            const uint64_t b = (uint64_t)load_u32_any(kl + k) | ((uint64_t)load_u32_any(kl + k + 4) << 32);
+            if ((r64((k0 + k + mis) & 127u) ^ b) & m) return false;
+        }
+        return true;
     }
     AJX_COLD bool key_rest_equal(uint32_t k0, uint32_t cnt, const uint8_t* kl) const {
         for (uint32_t k = 0; k < cnt; k++)
@@ -543,6 +573,7 @@ struct Walk {
             T &= T - 1u;
             const uint32_t p = (uint32_t)(c.base + (int32_t)i);
             if (skipw) {
+                AJX_LEAN_TRACE(0);
                 if ((c.op >> i) & 1u) {
                     skipw++;
                 } else if (((--skipw) & 0xFFFFFFu) == 0) {
@@ -556,6 +587,7 @@ struct Walk {
                 const bool kq = (cok >> i) & 1u;
                 if (depth == 0 || (tarr && kq)) { st = S_SLOW; T = 0; break; }
                 if (tarr) {  // a string element
+                    AJX_LEAN_TRACE(1);
                     const uint32_t node = elem_node();
                     const int32_t s = leaf_sel(node);
                     if (s >= 0 || ea) {
@@ -567,6 +599,7 @@ struct Walk {
                     continue;
                 }
                 if (!expk) {  // the pending value string of a key
+                    AJX_LEAN_TRACE(2);
                     if (kq) { st = S_SLOW; T = 0; break; }
                     const int32_t s = leaf_sel(pend >> 24);
                     const uint32_t ps = pend & 0xFFFFFFu;
@@ -588,6 +621,7 @@ struct Walk {
                 // its value at p + 2
                 const uint32_t vs = p + 2, vb = rb(vs);
                 const uint32_t rv = vs - (uint32_t)c.base;  // 2..33
+                AJX_LEAN_TRACE(vb == '"' ? 3 : (vb == '{' || vb == '[') ? 4 : 5);
                 if (vb == '"') {
                     const uint64_t cq = ((uint64_t)c.cq | ((uint64_t)l.cq << 32)) & (~0ull << (rv + 1));
                     if (cq) {
@@ -615,6 +649,7 @@ struct Walk {
                 continue;
             }
             if ((c.op >> i) & 1u) {
+                AJX_LEAN_TRACE(depth == 0 ? 6 : 7);
                 if (depth == 0) {  // the root
                     if (p != 0) { st = S_SLOW; T = 0; break; }
                     open(0, rb(p) == '[', p);
@@ -628,11 +663,13 @@ struct Walk {
                 continue;
             }
             if ((c.cl >> i) & 1u) {
+                AJX_LEAN_TRACE(8);
                 if (depth == 0 || tarr != (rb(p) == ']' ? 1u : 0u) || (!tarr && !expk)) { st = S_SLOW; T = 0; break; }
                 close(p);
                 if (st != S_RUN) { T = 0; break; }
                 continue;
             }
+            AJX_LEAN_TRACE(9);
             if (ea) eager_elem(false, 0, 0, false);
             // an array element's scalar
             if (depth == 0 || !tarr) { st = S_SLOW; T = 0; break; }
@@ -649,14 +686,23 @@ struct Walk {
 // `load(b, nblk)` returns aligned 16-byte block b of the document (zeros past nblk). Returns
 // true when the capture row is valid (false: the exact scan decides the request); dec[0] /
 // dec[1]: the patterns decided while capturing / those of them that are true.
-template <class LoadBlock>
+// ABL (profiling ablations, kernel modes 15..18; the row then holds a checksum): 1 loads and
+// ring stores only, 2 + classification, 3 + the walk without eager patterns, 4 = stage A.
+// keep: every capture goes to the row (a caller reads the rows after the kernel), else
+// only those stage B needs.
+template <int ABL = 0, class LoadBlock>
 AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, uint32_t n, RowRef row, uint8_t* ring,
-                     uint32_t lane, LoadBlock load, uint64_t dec[2]) {
+                     uint32_t lane, LoadBlock load, uint64_t dec[2], uint32_t keep = 1) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
     Walk w;
-    w.tn = unip(tab.tn);
-    w.ks = unip(tab.ks);
-    w.lits = unip(blob + h->off_literals);
+    // the tables as the blob pointer plus uniform offsets: the offsets go to scalar registers
+    // and the pointers keep the blob's provenance, so that with the blob staged in LDS every
+    // table read is a ds_read (a pointer made uniform through an integer would be generic:
+    // flat loads, which wait for the document's loads in flight as well)
+    (void)tab;
+    w.tn = reinterpret_cast<const TrieNode*>(blob + uni(h->off_trie_nodes));
+    w.ks = reinterpret_cast<const KeySlot*>(blob + uni(h->off_key_slots));
+    w.lits = blob + uni(h->off_literals);
     w.ks_mask = uni((1u << h->key_slots_log2) - 1u);
     w.ks_probes = uni(h->key_probes);
     w.ks_mult = uni(h->key_mult);
@@ -681,9 +727,10 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     w.carry_oq = 0;
     w.lbs1 = 0;
     w.found = 0;
-    w.eg = uni(h->off_eager) ? unip(reinterpret_cast<const EagerSel*>(blob + uni(h->off_eager))) : nullptr;
+    w.eg = ABL != 3 && uni(h->off_eager) ? reinterpret_cast<const EagerSel*>(blob + uni(h->off_eager)) : nullptr;
     w.eT = w.eD = 0;
     w.ea = 0;
+    w.keep = keep;
     Carry cr;
     cr.f = 0;
     cr.bad = 0x7FFFFFFF;
@@ -710,6 +757,7 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     for (int j = 0; j < 4; j++) nxt[j] = load((uint32_t)j, nblk);
     put(0, nxt);
     Sub s0, s1, s2;
+    uint32_t ck = 0;  // (ablations: a checksum that keeps the skipped work's inputs live)
     {
         const uint32_t x0[8] = {nxt[0].x, nxt[0].y, nxt[0].z, nxt[0].w, nxt[1].x, nxt[1].y, nxt[1].z, nxt[1].w};
         classify(s0, x0, -(int32_t)mis, valid_of(-(int32_t)mis), cr);
@@ -722,6 +770,27 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
         if (more) {
 #pragma unroll
             for (int j = 0; j < 4; j++) nxt[j] = load((win + 1) * 4u + (uint32_t)j, nblk);
+        }
+        if constexpr (ABL == 1) {
+            if (more) {
+                put(((win + 1) & 1u) * 2u, nxt);
+                ck ^= nxt[0].x ^ nxt[1].y ^ nxt[2].z ^ nxt[3].w;
+            }
+            continue;
+        }
+        if constexpr (ABL == 2) {
+            if (more) {
+                const uint32_t slot2 = ((win + 1) & 1u) * 2u;
+                put(slot2, nxt);
+                const uint32_t x2[8] = {nxt[0].x, nxt[0].y, nxt[0].z, nxt[0].w, nxt[1].x, nxt[1].y, nxt[1].z, nxt[1].w};
+                classify(s2, x2, b0 + 64, valid_of(b0 + 64), cr);
+                const Block16 h0 = *reinterpret_cast<const Block16*>(ring + w.ro(slot2 * 32u + 32u));
+                const Block16 h1 = *reinterpret_cast<const Block16*>(ring + w.ro(slot2 * 32u + 48u));
+                const uint32_t x3[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+                classify(s1, x3, b0 + 96, valid_of(b0 + 96), cr);
+                ck ^= s2.tok ^ s2.bs ^ s1.tok ^ s1.bs;
+            }
+            continue;
         }
         w.walk(s0, s1);
         if (w.st != S_RUN) break;
@@ -744,6 +813,11 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
             classify(s1, x3, b0 + 96, valid_of(b0 + 96), cr);
         }
         s0 = s2;
+    }
+    if constexpr (ABL == 1 || ABL == 2) {
+        row[0] = (uint64_t)ck ^ ((uint64_t)(uint32_t)cr.bad << 32) ^ s0.tok ^ s1.tok;
+        dec[0] = dec[1] = 0;
+        return true;
     }
     if (w.st != S_DONE || cr.bad <= (int32_t)w.pend) {  // (pend: the root's close)
         row[0] = kRowSlow;

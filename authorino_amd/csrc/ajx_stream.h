@@ -205,10 +205,13 @@ AJX_HD Tabs tabs_of(const uint8_t* blob) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     const StreamHdr* s = reinterpret_cast<const StreamHdr*>(blob + h->off_stream);
     Tabs t;
-    t.ks = lean::unip(reinterpret_cast<const StreamKeySlot*>(blob + s->off_keys));
-    t.ps = lean::unip(reinterpret_cast<const StreamPathSlot*>(blob + s->off_paths));
-    t.eg = h->off_eager ? lean::unip(reinterpret_cast<const EagerSel*>(blob + h->off_eager)) : nullptr;
-    t.lits = lean::unip(blob + h->off_literals);
+    // (blob plus uniform offsets, not pointers made uniform through integers: a staged blob's
+    // tables are then read with ds_reads, not flat loads that also wait for the stream's
+    // document loads in flight)
+    t.ks = reinterpret_cast<const StreamKeySlot*>(blob + lean::uni(s->off_keys));
+    t.ps = reinterpret_cast<const StreamPathSlot*>(blob + lean::uni(s->off_paths));
+    t.eg = lean::uni(h->off_eager) ? reinterpret_cast<const EagerSel*>(blob + lean::uni(h->off_eager)) : nullptr;
+    t.lits = blob + lean::uni(h->off_literals);
     t.k_log2 = lean::uni(s->key_log2);
     t.k_mult = lean::uni(s->key_mult);
     t.k_probes = lean::uni(s->key_probes);

@@ -204,6 +204,14 @@ def _lean_decl():
     return L
 
 
+def lean_keep(keep: bool) -> None:
+    """keep False: the lean scan writes only the capture records stage B needs (the
+    kernel's default when no caller reads the rows); True: every record."""
+    L = lib()
+    L.ht_lean_keep.argtypes = [C.c_int]
+    L.ht_lean_keep(1 if keep else 0)
+
+
 def eval_lean(hr: "HostRuleset", doc, mis: int = 0, n_sel: int = 0):
     """The lean single-pass scan (ajx_lean.h) + stage B on the host: (tri | -1 exact scan |
     -2 not eligible, err, res, capture row or None)."""

@@ -119,7 +119,7 @@ hipError_t launch_select_rows(const uint8_t* const*, const uint8_t*, const uint6
 hipError_t launch_eval_fast(const uint8_t* const*, const uint32_t*, uint32_t, const uint8_t*, const uint64_t*,
                             const uint32_t*, uint32_t n, uint8_t* tri, int32_t* err, uint64_t* bm, uint32_t stride,
                             uint64_t* rows, uint32_t row_stride, uint32_t* slow_count, uint32_t*, hipStream_t, int,
-                            const uint32_t*, bool) {
+                            const uint32_t*, bool, bool) {
     *slow_count = n / 7;
     for (uint32_t r = 0; r < n; r++) rows[(size_t)r * row_stride] = r;
     results(n, tri, err, bm, stride);

@@ -262,6 +262,10 @@ extern "C" void ht_lean_last_dec(uint64_t* out) {
     out[0] = g_last_dec[0];
     out[1] = g_last_dec[1];
 }
+// keep = 0: the lean scan writes only the capture records stage B needs (the kernel's
+// default when no caller reads the rows); 1 every record
+static uint32_t g_lean_keep = 1;
+extern "C" void ht_lean_keep(int keep) { g_lean_keep = keep ? 1u : 0u; }
 extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
                                 uint64_t* row_out) {
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
@@ -281,7 +285,8 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
         return Block16{0, 0, 0, 0};
     };
     uint64_t dec[2] = {0, 0};
-    const bool ok = lean::scan_doc(blob, blob_tables(blob), d, len, row.data(), ring_mem, (uint32_t)mis * 5u, load, dec);
+    const bool ok =
+        lean::scan_doc(blob, blob_tables(blob), d, len, row.data(), ring_mem, (uint32_t)mis * 5u, load, dec, g_lean_keep);
     g_last_dec[0] = dec[0];
     g_last_dec[1] = dec[1];
     if (!ok) return -1;
@@ -312,6 +317,16 @@ extern "C" void ht_lean_classes(const uint8_t* bytes, uint32_t* out) {
     for (uint32_t c = 0; c < 8; c++) out[c] = d[lean::creg(c)];
 }
 
+// the lean walk's trace of the next scans (sub-window << 8 | token kind per iteration, see
+// AJX_LEAN_TRACE) into buf[cap]; returns the entries written so far (buf null: stop)
+extern "C" uint32_t ht_lean_trace(uint32_t* buf, uint32_t cap) {
+    const uint32_t n = lean::g_lean_trace_n;
+    lean::g_lean_trace = buf;
+    lean::g_lean_trace_cap = cap;
+    lean::g_lean_trace_n = 0;
+    lean::g_lean_subs = 0;
+    return n;
+}
 extern "C" void ht_lean_counts(uint64_t* iters, uint64_t* subs) {
     *iters = lean::g_lean_iters;
     *subs = lean::g_lean_subs;
