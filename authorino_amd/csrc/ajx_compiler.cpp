@@ -748,14 +748,15 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         std::vector<KeySlot> slots, best_slots;
         uint32_t probes = 0xFFFFFFFFu, best_log2 = log2, mult = 0x9E3779B1u;
         auto build = [&](uint32_t lg, uint32_t m, std::vector<KeySlot>& out) -> uint32_t {
-            out.assign(1u << lg, KeySlot{0, kEmptySlot, 0});
+            out.assign(1u << lg, KeySlot{0, kEmptySlot, 0, 0});
             uint32_t worst = 1;
             for (const Ent& e : ents) {
                 uint32_t at = key_slot_hash(e.sig, e.len, e.parent, lg, m), dist = 1;
                 while (out[at].meta != kEmptySlot) at = (at + 1) & ((1u << lg) - 1), dist++;
                 out[at].sig = e.sig;
                 out[at].meta = e.len | (e.parent << 16) | (e.node << 24);
-                out[at].key_off = e.key_off;
+                out[at].key_off8 = (uint16_t)(e.key_off / 8u);  // (a pool past 512 KiB: no fast path, below)
+                out[at].info = (uint16_t)node_info(tn[e.node]);
                 worst = std::max(worst, dist);
             }
             return worst;
@@ -816,8 +817,12 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             if (any) {
                 hdr.off_eager = (uint32_t)b.align16();
                 b.append(eg.data(), eg.size() * sizeof(EagerSel));
-                // (the trie nodes were appended before their eager flags were set: rewrite)
+                // (the trie nodes and key slots were appended before the eager flags were
+                // set: rewrite)
                 std::memcpy(b.blob.data() + hdr.off_trie_nodes, tn.data(), tn.size() * sizeof(TrieNode));
+                for (KeySlot& sl : slots)
+                    if (sl.meta != kEmptySlot) sl.info = (uint16_t)node_info(tn[sl.meta >> 24]);
+                std::memcpy(b.blob.data() + hdr.off_key_slots, slots.data(), slots.size() * sizeof(KeySlot));
             }
         }
         // streaming scan tables (ajx_stream.h): key ids, and the selectors by their
@@ -1076,6 +1081,8 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     hdr.max_depth = max_depth;
     hdr.lit_bytes = (uint32_t)lits.size();
     hdr.n_components = (uint32_t)comps.size();
+    // (KeySlot::key_off8 reaches 512 KiB of literal pool)
+    if (lits.size() >= 8u * 65536u) flags &= ~kFlagFastOk;
     hdr.flags = flags;
     std::memcpy(b.blob.data(), &hdr, sizeof hdr);
     out->blob = std::move(b.blob);

@@ -386,7 +386,7 @@ struct Scan {
             const KeySlot slot = ks[pos];
             if (slot.meta == kEmptySlot) return;
             if (slot.sig != sig || (slot.meta & 0xFFFFFFu) != want) continue;
-            if (klen <= 8 || key_rest_equal(k0, klen, slot.key_off)) { pending = slot.meta >> 24; return; }
+            if (klen <= 8 || key_rest_equal(k0, klen, (uint32_t)slot.key_off8 * 8u)) { pending = slot.meta >> 24; return; }
         }
     }
     // the bytes of a key [k0, k0 + klen) before its last 8 equal the literal at key_off

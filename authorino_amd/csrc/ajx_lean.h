@@ -419,7 +419,7 @@ struct Walk {
             const KeySlot sl = ks[(h + t) & ks_mask];
             bool hit = sl.meta != kEmptySlot && sl.sig == sig && (sl.meta & 0xFFFFFFu) == want;
             // (keys sharing their last 8 bytes, length and parent sit in later slots)
-            if (hit && longk) hit = key_head_equal(kstart, len - 8, lits + sl.key_off);
+            if (hit && longk) hit = key_head_equal(kstart, len - 8, lits + (uint32_t)sl.key_off8 * 8u);
             node = hit ? sl.meta >> 24 : node;
         }
         return node;
@@ -611,13 +611,12 @@ struct Walk {
                 // a key: [ks, p)
                 const uint32_t ks0 = (c.oq & below(i)) ? (uint32_t)c.base + hib(c.oq & below(i)) : carry_oq;
                 const uint32_t k0 = ks0 + 1, klen = p - k0;
-                uint32_t node = kNoNode;
-                if (top != kNoNode && tn[top].n_children) {
-                    if (klen >= kIdxKeyLen || has_bs(k0, p, c, l)) { st = S_SLOW; T = 0; break; }
-                    uint64_t sig = r64((p - 8u + mis) & 127u);
-                    sig = klen >= 8 ? sig : (klen ? sig >> (8 * (8 - klen)) : 0ull);
-                    node = lookup(sig, klen, top, k0);
-                }
+                // (every object the walk is in has keys on selector paths: open() squashes
+                // the others)
+                if (klen >= kIdxKeyLen || has_bs(k0, p, c, l)) { st = S_SLOW; T = 0; break; }
+                uint64_t sig = r64((p - 8u + mis) & 127u);
+                sig = klen >= 8 ? sig : (klen ? sig >> (8 * (8 - klen)) : 0ull);
+                const uint32_t node = lookup(sig, klen, top, k0);
                 // its value at p + 2
                 const uint32_t vs = p + 2, vb = rb(vs);
                 const uint32_t rv = vs - (uint32_t)c.base;  // 2..33

@@ -29,6 +29,8 @@ KINDS = ["squash", "str_elem", "pend_val", "key_str", "key_cont", "key_scalar", 
 # rough per-kind cost in wave instructions (VALU + SALU) of the branch body
 COST = [20, 90, 60, 140, 120, 110, 40, 100, 50, 90]
 OVERHEAD = 30  # loop head: ctz, bit clear, dispatch tests
+KIND_ITERS = collections.Counter()  # iterations in which some lane runs each kind
+NKINDS = []
 
 
 def traces(expr, docs):
@@ -70,6 +72,8 @@ def wave_costs(wave, window=1):
         for j in range(m):
             present = {q[j] for q in seqs if j < len(q)}
             lock += OVERHEAD + sum(COST[k] for k in present)
+            KIND_ITERS.update(present)
+            NKINDS.append(len(present))
         heads = [0] * len(seqs)
         while True:
             c = collections.Counter(q[h] for q, h in zip(seqs, heads) if h < len(q))
@@ -109,6 +113,8 @@ def main():
                     "waves": 1})
     nw = tot["waves"]
     print({k: round(v / nw, 1) for k, v in tot.items()})
+    print("kinds per lockstep iteration:", round(float(np.mean(NKINDS)), 2),
+          "iterations per wave running each kind:", {KINDS[k]: round(v / nw / 2, 1) for k, v in KIND_ITERS.items()})
 
 
 if __name__ == "__main__":

@@ -139,3 +139,55 @@ def test_stream_counters_across_launches(ctx):
     ctx.set_stream_max(4096)
     stream_counts = [c for c, m in zip(counts, (1, 1, 0, 1, 1)) if m]
     assert stream_counts[0] > 0 and len(set(stream_counts)) == 1, counts
+
+
+def _dense_docs(rng, n):
+    """Documents whose 32-byte blocks hold many opens and keys: nested arrays and objects
+    with one-letter keys (`[[[[[[[[[[1]]]]]]]]]]`, `{"a":{"b":{"c":...`), so a block has
+    more than 8 opens (the capture loop's open ordinals: round 4's out-of-range
+    `oids >> (8 * no)` for no >= 8) and runs of short keys."""
+    out = []
+    for _ in range(n):
+        k = int(rng.integers(6, 20))
+        arr = "[" * k + str(int(rng.integers(0, 9))) + "]" * k
+        keys = "abcdefghij"
+        obj = "".join('{"%s":' % keys[j % 10] for j in range(k)) + '"v"' + "}" * k
+        flat = "{" + ",".join('"%s":%d' % (keys[j], j) for j in range(10)) + "}"
+        parts = [('"x"', arr), ('"y"', obj), ('"z"', flat)]
+        rng.shuffle(parts)
+        out.append(("{" + ",".join("%s:%s" % p for p in parts) + "}").encode())
+    return out
+
+
+@pytest.mark.parametrize("n", [1, 64, 2000])
+def test_stream_dense_blocks(ctx, n):
+    """Regression for round 4's launch failures on one-request batches: blocks with more
+    than 8 opens / many keys, selectors into them (array indices, deep keys), at 1, 64 and
+    2000 requests per batch; every result the oracle's."""
+    rng = np.random.default_rng(94 + n)
+    pats = [("x.0.0.0", 1, "[[[1]]]"), ("y.a.b.c", 3, "v"), ("z.j", 1, "9"), ("z.a", 2, "0"),
+            ("y.a.b.c.d.e.f.g", 1, "v"), ("x.0.0.0.0.0.0.0.0", 1, "3")]
+    nodes, root = FU.chain(len(pats))
+    _same(ctx, [(pats, nodes, root)], *_pack(_dense_docs(rng, n)))
+
+
+def test_stream_slow_path_batch_latency(ctx):
+    """a 4096-request small batch whose documents all leave the stream (nesting
+    deeper than it tracks, documents over one step) goes through the grid-stride stage-B
+    launch, not one wave's list: results equal to the oracle, and the batch takes at most
+    a few milliseconds."""
+    import time
+
+    deep = b'{"a":' + b'{"b":' * 20 + b'"v"' + b"}" * 20 + b',"c":"' + b"p" * 2100 + b'","d":"w"}'
+    docs = [deep] * 4096
+    pats = [("d", 1, "w"), ("c", 2, "x"), ("a.b.b", 3, "v")]
+    nodes, root = FU.chain(len(pats))
+    arena, offs, lens = _pack(docs)
+    rs = ctx.compile(pats, nodes, root)
+    ctx.eval_host_arena([rs], arena, offs, lens)  # (warm up)
+    t0 = time.perf_counter()
+    tri, _, _ = ctx.eval_host_arena([rs], arena, offs, lens)
+    dt = time.perf_counter() - t0
+    otri, _, _ = O.eval_batch([O.Ruleset(pats, nodes, root)], arena, offs, lens, nthreads=8)
+    assert np.array_equal(tri, otri)
+    assert dt < 0.05, dt

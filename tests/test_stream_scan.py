@@ -198,3 +198,16 @@ def test_stream_empty_and_tiny_documents():
     docs = [b"", b"{}", b"[]", b'{"a":1}', b"1", b'"a"', b"{", b'{"a":1}' * 2, b'{"a":[]}', b'{"b":["x"]}',
             b'{"a":[1,2\x01]}', b'{"b":[1\x01,"x"]}', b'{"b":"x\x01"}']
     _check(pats, nodes, root, *_pack(docs))
+
+
+@pytest.mark.parametrize("per", [1, 32])
+def test_stream_dense_blocks(per):
+    """Blocks with more than 8 opens and runs of one-letter keys (the capture loop's open /
+    key ordinals; tests/test_gpu_stream.py runs the same documents on the device)."""
+    from test_gpu_stream import _dense_docs
+
+    rng = np.random.default_rng(95 + per)
+    pats = [("x.0.0.0", 1, "[[[1]]]"), ("y.a.b.c", 3, "v"), ("z.j", 1, "9"), ("z.a", 2, "0"),
+            ("y.a.b.c.d.e.f.g", 1, "v"), ("x.0.0.0.0.0.0.0.0", 1, "3")]
+    nodes, root = FU.chain(len(pats))
+    _check(pats, nodes, root, *_pack(_dense_docs(rng, 96)), per=per)
