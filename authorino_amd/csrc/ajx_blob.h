@@ -158,19 +158,9 @@ struct KeySlot {
     uint64_t sig;       // key_signature(key)
     uint32_t meta;      // key_len | parent << 16 | node << 24; kEmptySlot = free
     uint16_t key_off8;  // key bytes in the literal pool, / 8 (keys are 8-byte aligned)
-    uint16_t info;      // the child node's walk facts (kInfo*), so that the lean walk reads no
-                        // trie node after a lookup
+    uint16_t pad;
 };
 static_assert(sizeof(KeySlot) == 16, "KeySlot layout");
-// KeySlot::info: the node's selector (kInfoNoSel: none), whether it has children, a leaf
-// with eager incl / excl patterns (TrieNode flags bit 1), children that are array indices
-// (flags bit 0)
-constexpr uint32_t kInfoSel = 0x7Fu, kInfoNoSel = 0x7Fu, kInfoKids = 1u << 7, kInfoEager = 1u << 8,
-                   kInfoIdx = 1u << 9;
-AJX_BLOB_HD inline uint32_t node_info(const TrieNode& t) {
-    return (t.selector < 0 ? kInfoNoSel : (uint32_t)t.selector & kInfoSel) | (t.n_children ? kInfoKids : 0u) |
-           ((t.flags & 2) ? kInfoEager : 0u) | ((t.flags & 1) ? kInfoIdx : 0u);
-}
 constexpr uint32_t kEmptySlot = 0xFFFFFFFFu;
 constexpr uint32_t kMaxKeySlotsLog2 = 9;
 constexpr uint32_t kKeyProbes = 4;  // the table is grown until every key is this close to home

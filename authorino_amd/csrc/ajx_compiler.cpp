@@ -756,7 +756,6 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 out[at].sig = e.sig;
                 out[at].meta = e.len | (e.parent << 16) | (e.node << 24);
                 out[at].key_off8 = (uint16_t)(e.key_off / 8u);  // (a pool past 512 KiB: no fast path, below)
-                out[at].info = (uint16_t)node_info(tn[e.node]);
                 worst = std::max(worst, dist);
             }
             return worst;
@@ -817,12 +816,8 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             if (any) {
                 hdr.off_eager = (uint32_t)b.align16();
                 b.append(eg.data(), eg.size() * sizeof(EagerSel));
-                // (the trie nodes and key slots were appended before the eager flags were
-                // set: rewrite)
+                // (the trie nodes were appended before their eager flags were set: rewrite)
                 std::memcpy(b.blob.data() + hdr.off_trie_nodes, tn.data(), tn.size() * sizeof(TrieNode));
-                for (KeySlot& sl : slots)
-                    if (sl.meta != kEmptySlot) sl.info = (uint16_t)node_info(tn[sl.meta >> 24]);
-                std::memcpy(b.blob.data() + hdr.off_key_slots, slots.data(), slots.size() * sizeof(KeySlot));
             }
         }
         // streaming scan tables (ajx_stream.h): key ids, and the selectors by their

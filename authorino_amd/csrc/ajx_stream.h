@@ -592,6 +592,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                 }
                 if (id) keym |= 1u << i;
                 if (nk < 8) kids |= (uint64_t)id << (8u * nk);
+                if (nk == 8) bad |= 1u << i;  // (a 9th key in the block: exact scan, see below)
                 nk++;
                 last_kid = id;
                 if (i == 31) kid31 = id;
@@ -626,6 +627,7 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
                 else if (pend_lvl == (uint32_t)dd)
                     pend_lvl = 0;
                 if (no < 8) oids |= (uint64_t)id << (8u * no);
+                if (no == 8) bad |= 1u << i;  // (a 9th open in the block: exact scan, see below)
                 no++;
                 if (dd >= 2 && dd <= 9) {
                     const uint32_t sh = 8u * ((uint32_t)(dd - 2) & 3u);
@@ -649,7 +651,11 @@ AJX_HD void step(WaveLds& L, uint64_t* rows, const Tabs& T, uint32_t t, uint32_t
             }
         }
         segment(31u);
-        if (nk > 8 || no > 8) bad |= 1u;  // (keys take at least 4 bytes; 9 opens in 32 bytes: exact scan)
+        // (the capture loop keeps the ids of 8 keys and 8 opens per block: a 9th of either
+        // sends the document to the exact scan, marked at its own position above. Not at the
+        // block's byte 0: in a document's first block that byte can lie before the document,
+        // where the mark would be lost and a selector under the 9th open missed; found by
+        // tests/test_gpu_stream.py::test_stream_dense_blocks)
     }
     // the id of a key whose ':' ended the lane before (or the step before)
     {

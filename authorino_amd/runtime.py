@@ -511,6 +511,10 @@ class BatchTimeout(AuthjxError):
     """The request's deadline passed before its batch was evaluated (AUTHJX_ETIMEDOUT)."""
 
 
+_batcher_knob_lock = threading.Lock()
+_BATCHER_DEFAULT_WORKERS = 2  # (ajx_api.cpp g_batcher_workers' default; only this module changes it)
+
+
 class Batcher:
     """The micro-batcher (authjx_batcher_*): many threads call eval() with one request
     each; the native worker forms batches (size / window flush, deadlines, AuthConfig
@@ -522,16 +526,20 @@ class Batcher:
         """workers: worker threads, each with its own stream (0: the library's default, 2;
         profiling knob, authjx_debug_batcher_workers, not part of authjx.h)."""
         L = load_library()
-        if workers:
-            L.authjx_debug_batcher_workers.argtypes = [C.c_uint32]
-            _check(L.authjx_debug_batcher_workers(int(workers)), "authjx_debug_batcher_workers")
         h = C.c_void_p()
-        try:
-            _check(L.authjx_batcher_create(ctx._h, max_batch, window_us, queue_cap, C.byref(h)),
-                   "authjx_batcher_create")
-        finally:
+        # (the worker count is a process-wide knob of the library that batcher creation
+        # reads: set, create and restore under one lock, so that batchers created at the
+        # same time in other threads keep the count they asked for)
+        with _batcher_knob_lock:
             if workers:
-                L.authjx_debug_batcher_workers(2)
+                L.authjx_debug_batcher_workers.argtypes = [C.c_uint32]
+                _check(L.authjx_debug_batcher_workers(int(workers)), "authjx_debug_batcher_workers")
+            try:
+                _check(L.authjx_batcher_create(ctx._h, max_batch, window_us, queue_cap, C.byref(h)),
+                       "authjx_batcher_create")
+            finally:
+                if workers:
+                    L.authjx_debug_batcher_workers(_BATCHER_DEFAULT_WORKERS)
         self.ctx = ctx
         self._h = h
         ctx._batchers.add(self)

@@ -131,10 +131,12 @@ typedef struct {
 int authjx_init(int device, authjx_ctx** out);
 void authjx_shutdown(authjx_ctx* ctx);
 /* Release the per-stream workspace (capture rows, slow list, order, set table) the
- * context keeps for `stream` since its first device call on it, after that stream's last
- * batch: for callers that use short-lived streams. Not the context's own stream. A call
- * still running on that stream, or an authjx_last_* reader, keeps the workspace until it
- * returns (reference-counted); only authjx_shutdown must not race the context's calls. */
+ * context keeps for `stream` since its first device call on it: for callers that use
+ * short-lived streams. Not the context's own stream. The workspace is reference-counted:
+ * a call still running on that stream, or an authjx_last_* reader, keeps it until that
+ * call returns, and whichever thread drops the last reference (this one, or that call's)
+ * waits for the stream's last batch before freeing it, so this call may return before
+ * that batch has ended. Only authjx_shutdown must not race the context's calls. */
 int authjx_release_stream(authjx_ctx* ctx, void* stream);
 // The sha256 (first 32 hex digits) of the sources the library was built from
 // (authorino_amd/build.py source_hash); the Python runtime refuses a stale binary.
@@ -170,9 +172,10 @@ size_t authjx_pattern_error(const authjx_ruleset* rs, uint32_t i, char* buf, siz
  *   sets[n_sets]      rulesets; request r uses sets[set_of_req ? set_of_req[r] : 0]
  *   d_set_of_req      device u32[n] (entries < n_sets) or NULL; ignored when n_sets == 1
  *   d_arena           device bytes; document r = d_arena[d_offs[r] .. + d_lens[r]). The
- *                     kernels read whole aligned 16-byte blocks: every block holding a
- *                     document byte must be readable (device allocations are; an arena
- *                     carved from a larger buffer needs 15 readable bytes after its end)
+ *                     kernels read whole aligned 32-byte blocks (the streaming kernel's
+ *                     unit; the others read 16): every block holding a document byte must
+ *                     be readable (device allocations are; an arena carved from a larger
+ *                     buffer needs 31 readable bytes after its end)
  *   d_out_tristate    device u8[n * n_trees]  (AUTHJX_F/T/E/UNDECIDED; n_trees = 1 unless
  *                     the rulesets come from authjx_compile_forest)
  *   d_out_err_idx     device i32[n * n_trees] pattern whose error decided an E, else -1
