@@ -809,7 +809,10 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                     any = true;
                 }
                 if (all && k) eg[sidx].pad[0] = kEagerAll;
-                if (arr_ops)
+                // (the lean scan walks an array value element by element only when that
+                // decides every pattern of the selector: otherwise stage B walks it again
+                // for the others, and the scan squashes it instead)
+                if (arr_ops && all)
                     for (size_t i = 0; i < trie.size(); i++)
                         if (trie[i].selector == (int16_t)sidx) tn[i].flags |= 2;
             }
