@@ -123,8 +123,7 @@ constexpr uint8_t kNoNode = 0xFF;
 struct TrieNode {
     uint16_t child_begin;  // index into TrieChild[]
     uint8_t n_children;
-    uint8_t flags;         // bit0: has array-index children; bit1: a leaf with eager
-                           // incl/excl patterns (the lean scan walks its array value)
+    uint8_t flags;         // bit0: has array-index children
     int16_t selector;      // selector whose path ends here, -1 none
     uint16_t pad;
 };
@@ -226,9 +225,9 @@ constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the
 
 // Patterns the lean scan decides while it captures (ajx_lean.h): per selector, its first
 // two patterns (index < 64) that compare an unescaped string value's text with a literal
-// of at most 16 bytes (eq, neq, incl / excl on the value alone), and incl / excl over
-// an array of unescaped strings; a literal value (true / false / null) decides them by the
-// literal's litf. m: pattern | op << 8 | literal length << 16 | litf << 24 | 1 << 31.
+// of at most 16 bytes (eq, neq, incl / excl on the value alone); a literal value (true /
+// false / null) decides them by the literal's litf. (The streaming kernel also compares
+// arrays of strings with them, element by element.) m: pattern | op << 8 | literal length << 16 | litf << 24 | 1 << 31.
 // pad[0] bit 0 (kEagerAll): those are every pattern of the selector (a decided value needs
 // no capture record for stage B).
 struct EagerSel {

@@ -793,7 +793,7 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
             bool any = false;
             for (size_t sidx = 0; sidx < sels.size(); sidx++) {
                 uint32_t k = 0;
-                bool arr_ops = false, all = true;
+                bool all = true;
                 for (uint16_t pi : sel_pats[sidx]) {
                     const Pattern& pt = pats[pi];
                     if (k >= 2 || pi >= 64 || pt.state != P_OK || pt.lit_len > 16 ||
@@ -804,23 +804,15 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                     if (pt.lit_len) std::memcpy(eg[sidx].lit[k], lits.data() + pt.lit_off, pt.lit_len);
                     eg[sidx].m[k] = (uint32_t)pi | ((uint32_t)pt.op << 8) | (pt.lit_len << 16) |
                                     ((uint32_t)(pt.litf & 7u) << 24) | kEagerValid;
-                    arr_ops = arr_ops || pt.op == OP_INCL || pt.op == OP_EXCL;
                     k++;
                     any = true;
                 }
                 if (all && k) eg[sidx].pad[0] = kEagerAll;
-                // (the lean scan walks an array value element by element only when that
-                // decides every pattern of the selector: otherwise stage B walks it again
-                // for the others, and the scan squashes it instead)
-                if (arr_ops && all)
-                    for (size_t i = 0; i < trie.size(); i++)
-                        if (trie[i].selector == (int16_t)sidx) tn[i].flags |= 2;
+
             }
             if (any) {
                 hdr.off_eager = (uint32_t)b.align16();
                 b.append(eg.data(), eg.size() * sizeof(EagerSel));
-                // (the trie nodes were appended before their eager flags were set: rewrite)
-                std::memcpy(b.blob.data() + hdr.off_trie_nodes, tn.data(), tn.size() * sizeof(TrieNode));
             }
         }
         // streaming scan tables (ajx_stream.h): key ids, and the selectors by their

@@ -275,11 +275,12 @@ struct Walk {
     uint32_t carry_oq;      // last opening quote before the sub-window being walked
     uint32_t lbs1;          // last backslash before it, + 1 (0 none)
     uint64_t found;
-    // eager patterns (EagerSel, ajx_blob.h): decided (eD) and true (eT) bits of patterns < 64;
-    // ea: the open eager array (selector + 1 | depth << 8 | entry hits << 16 | dirty << 18)
+    // eager patterns (EagerSel, ajx_blob.h): decided (eD) and true (eT) bits of patterns < 64.
+    // (Arrays are not compared element by element: an array value is squashed and stage B
+    // decides its incl / excl patterns in one pass; comparing c2's two arrays in the walk
+    // measured the same, 1.408 against 1.418 ms, and cost the walk a branch per token)
     const EagerSel* eg;
     uint64_t eT, eD;
-    uint32_t ea;
     uint32_t keep;  // every capture record goes to the row (a caller reads the rows)
 
     AJX_HD uint32_t ro(uint32_t a) const { return ((a & 0x70u) ^ sw16) | (a & 15u); }  // ring offset a (0..127)
@@ -376,31 +377,6 @@ struct Walk {
         }
         return r;
     }
-    // an element of the open eager array: a string's content (hits), else the array is left
-    // to stage B
-    AJX_HD void eager_elem(bool str, uint32_t a, uint32_t cl, bool esc) {
-        if (!ea || (ea >> 8 & 0xFFu) != depth) return;
-        if (!str || esc) {
-            ea |= 1u << 18;
-            return;
-        }
-        ea |= eager_match(eg[(ea & 0xFFu) - 1u], a, cl) << 16;
-    }
-    AJX_HD void eager_close() {
-        if (!ea || (ea >> 8 & 0xFFu) != depth) return;
-        if (!((ea >> 18) & 1u)) {
-            const EagerSel e = eg[(ea & 0xFFu) - 1u];
-#pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const uint32_t m = e.m[k], op = (m >> 8) & 0xFFu;
-                if (!(m & kEagerValid) || (op != OP_INCL && op != OP_EXCL)) continue;
-                const uint64_t bit = 1ull << (m & 63u);
-                eD |= bit;
-                if (((ea >> (16 + k)) & 1u) == (op == OP_INCL ? 1u : 0u)) eT |= bit;
-            }
-        }
-        ea = 0;
-    }
     // the key table: (sig, len, parent) -> child node (kNoNode none). len = kIdxKeyLen:
     // sig is an array index. A hit on a key longer than 8 bytes also compares its head
     // (bytes [ks, len - 8) of the key, starting at doc position ks).
@@ -450,8 +426,7 @@ struct Walk {
     // a container value at p ('{' or '['), node = its trie node
     AJX_HD void open(uint32_t node, bool arr, uint32_t p) {
         const int32_t s = leaf_sel(node);
-        const bool eager = arr && eg && s >= 0 && !ea && (tn[node].flags & 2);  // (its elements compared)
-        if (node == kNoNode || (tn[node].n_children == 0 && !eager)) {  // squashed (captured when a leaf)
+        if (node == kNoNode || tn[node].n_children == 0) {  // squashed (captured when a leaf)
             skipw = 1u | ((s >= 0 ? (uint32_t)s + 1u : 0u) << 24);
             skips = p;
             return;
@@ -473,7 +448,6 @@ struct Walk {
         tarr = arr ? 1u : 0u;
         expk = 1;
         idx = 0;
-        if (eager) ea = ((uint32_t)s + 1u) | (depth << 8);
         if (s >= 0) {
             found |= 1ull << s;  // (first match in document order)
             if (ncap >= 2) { st = S_SLOW; return; }
@@ -485,7 +459,6 @@ struct Walk {
         }
     }
     AJX_HD void close(uint32_t p) {
-        eager_close();
         if (ncap) {
             const uint32_t cs = ncap == 2 ? caps >> 16 : caps & 0xFFFFu, start = ncap == 2 ? cap1s : cap0s;
             if ((cs >> 8) == depth) {
@@ -590,11 +563,10 @@ struct Walk {
                     AJX_LEAN_TRACE(1);
                     const uint32_t node = elem_node();
                     const int32_t s = leaf_sel(node);
-                    if (s >= 0 || ea) {
+                    if (s >= 0) {
                         const uint32_t so = (c.oq & below(i)) ? (uint32_t)c.base + hib(c.oq & below(i)) : carry_oq;
                         const bool esc = has_bs(so, p, c, l);
                         if (s >= 0) record(s, so, p + 1, T_STRING, esc ? 1u : 0u);
-                        if (ea) eager_elem(true, so + 1u, p - so - 1u, esc);
                     }
                     continue;
                 }
@@ -656,7 +628,6 @@ struct Walk {
                     continue;
                 }
                 if (!tarr) { st = S_SLOW; T = 0; break; }  // (a container where a key belongs)
-                if (ea) eager_elem(false, 0, 0, false);
                 open(elem_node(), rb(p) == '[', p);
                 if (skipw) T &= c.op | c.cl;
                 continue;
@@ -669,7 +640,6 @@ struct Walk {
                 continue;
             }
             AJX_LEAN_TRACE(9);
-            if (ea) eager_elem(false, 0, 0, false);
             // an array element's scalar
             if (depth == 0 || !tarr) { st = S_SLOW; T = 0; break; }
             const uint32_t node = elem_node();
@@ -728,7 +698,6 @@ AJX_HD bool scan_doc(const uint8_t* blob, const Tables& tab, const uint8_t* d, u
     w.found = 0;
     w.eg = ABL != 3 && uni(h->off_eager) ? reinterpret_cast<const EagerSel*>(blob + uni(h->off_eager)) : nullptr;
     w.eT = w.eD = 0;
-    w.ea = 0;
     w.keep = keep;
     Carry cr;
     cr.f = 0;
