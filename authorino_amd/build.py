@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libauthjx.so")
 INCLUDE_H = os.path.join(HERE, "..", "include", "authjx.h")
-SOURCES = ["ajx_regex.cpp", "ajx_compiler.cpp", "ajx_api.cpp", "ajx_index.cpp", "ajx_producer.cpp", "ajx_kernels.hip"]
+SOURCES = ["ajx_regex.cpp", "ajx_compiler.cpp", "ajx_api.cpp", "ajx_index.cpp", "ajx_producer.cpp", "ajx_kernels.hip", "ajx_lean.hip"]
 ARCH = os.environ.get("AUTHJX_ARCH", "gfx950")
 _INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
 
@@ -69,6 +69,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     # the hash is compiled into ajx_api.cpp: rebuilt whenever any source changed
     if stale and "ajx_api.cpp" not in stale:
         stale.append("ajx_api.cpp")
+    # every stale object compiled at once (the kernel translation units take minutes each)
+    procs = []
     for src in stale:
         obj = _obj(src)
         os.makedirs(os.path.dirname(obj), exist_ok=True)
@@ -76,7 +78,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
                f'-DAJX_SRC_HASH="{digest}"', "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        procs.append((subprocess.Popen(cmd), obj, cmd))
+    failed = [cmd for p, _, cmd in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    for _, obj, _ in procs:
         os.replace(obj + ".tmp", obj)
     if stale or not os.path.exists(OUT):
         tmp = OUT + ".tmp"

@@ -567,7 +567,8 @@ static int eval_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint3
     const bool full = ablate == 0 || ablate == 41 || ablate == 52 || (ablate >= 10 && ablate <= 12) ||
                       (ablate >= 15 && ablate <= 18);  // (15..18: lean ablations, length order kept)
     const auto* h0 = reinterpret_cast<const ajx::RulesetHdr*>(sets[0]->c.blob.data());
-    const bool keep_rows = !force_scan && n_sets == 1 && full && h0->pad1[0] != 0;
+    // (not under the lean ablations 15..18: their rows hold checksums)
+    const bool keep_rows = !force_scan && n_sets == 1 && full && !(ablate >= 15 && ablate <= 18) && h0->pad1[0] != 0;
     w->rows_rs = keep_rows ? sets[0] : nullptr;
     w->rows_n = n;
     w->rows_stride = row_stride;
@@ -687,8 +688,19 @@ int authjx_select_from_eval_device(authjx_ctx* ctx, const authjx_ruleset* rs, ui
     Workspace* w = wl.w;
     if (!w) return AUTHJX_EDEVICE;
     // the rows must be this stream's last evaluation's, of this ruleset, over this many
-    // requests
+    // requests, and hold these patterns' records: a selector the scan decides eagerly has a
+    // record only when it belongs to a root-less tree of the forest (kEagerKeep)
     if (w->rows_rs != rs || w->rows_n != n) return AUTHJX_EINVAL;
+    {
+        const auto* h = reinterpret_cast<const ajx::RulesetHdr*>(rs->c.blob.data());
+        const auto* pats = reinterpret_cast<const ajx::Pattern*>(rs->c.blob.data() + h->off_patterns);
+        const auto* eg = h->off_eager ? reinterpret_cast<const ajx::EagerSel*>(rs->c.blob.data() + h->off_eager)
+                                      : nullptr;
+        for (uint32_t p = first_pattern; eg && p < first_pattern + values_stride; p++) {
+            const uint32_t f = eg[pats[p].selector].pad[0];
+            if ((f & ajx::kEagerAll) && !(f & ajx::kEagerKeep)) return AUTHJX_EINVAL;
+        }
+    }
     hipStream_t s = w->stream;
     HIP_OK(hipSetDevice(ctx->device));
     const authjx_ruleset* one[1] = {rs};

@@ -229,7 +229,9 @@ constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the
 // false / null) decides them by the literal's litf. (The streaming kernel also compares
 // arrays of strings with them, element by element.) m: pattern | op << 8 | literal length << 16 | litf << 24 | 1 << 31.
 // pad[0] bit 0 (kEagerAll): those are every pattern of the selector (a decided value needs
-// no capture record for stage B).
+// no capture record for stage B); bit 1 (kEagerKeep): a selector of a forest's root-less
+// tree, whose record a caller reads back (authjx_select_from_eval_device): written whenever
+// the kernel keeps rows.
 struct EagerSel {
     uint32_t lit[2][4];
     uint32_t m[2];
@@ -238,6 +240,7 @@ struct EagerSel {
 static_assert(sizeof(EagerSel) == 48, "EagerSel layout");
 constexpr uint32_t kEagerValid = 1u << 31;  // EagerSel::m[k] holds an eager pattern
 constexpr uint32_t kEagerAll = 1u;           // EagerSel::pad[0]
+constexpr uint32_t kEagerKeep = 2u;          // EagerSel::pad[0]
 
 // ---- streaming scan (ajx_stream.h) ------------------------------------------------
 // The stream resolves object keys without their parent: every distinct object key of the

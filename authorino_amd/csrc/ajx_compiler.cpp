@@ -393,7 +393,7 @@ struct Builder {
 
 namespace {
 int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, bool forest, CompiledRuleset* out,
-                 std::string* err);
+                 std::string* err, const std::vector<uint8_t>* kept = nullptr);
 }
 
 int compile_tree(const authjx_tree* tree, CompiledRuleset* out, std::string* err) {
@@ -409,12 +409,14 @@ int compile_forest(const authjx_tree* trees, uint32_t n_trees, CompiledRuleset* 
     std::vector<authjx_pattern> pats;
     std::vector<authjx_node> nodes;
     std::vector<int32_t> roots;
+    std::vector<uint8_t> kept;  // patterns of root-less trees: selectors a caller reads back
     for (uint32_t k = 0; k < n_trees; k++) {
         const authjx_tree& t = trees[k];
         if ((t.n_patterns && !t.patterns) || (t.n_nodes && !t.nodes) || t.root >= (int32_t)t.n_nodes)
             return AUTHJX_EINVAL;
         const int32_t po = (int32_t)pats.size(), no = (int32_t)nodes.size();
         pats.insert(pats.end(), t.patterns, t.patterns + t.n_patterns);
+        kept.insert(kept.end(), t.n_patterns, t.root < 0 ? 1 : 0);
         for (uint32_t i = 0; i < t.n_nodes; i++) {
             authjx_node nd = t.nodes[i];
             if (nd.left >= (int32_t)t.n_nodes || nd.right >= (int32_t)t.n_nodes) return AUTHJX_EINVAL;
@@ -428,12 +430,12 @@ int compile_forest(const authjx_tree* trees, uint32_t n_trees, CompiledRuleset* 
         roots.push_back(t.root < 0 ? -1 : t.root + no);
     }
     authjx_tree all{pats.data(), (uint32_t)pats.size(), nodes.data(), (uint32_t)nodes.size(), -1};
-    return compile_core(&all, roots, true, out, err);
+    return compile_core(&all, roots, true, out, err, &kept);
 }
 
 namespace {
 int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, bool forest, CompiledRuleset* out,
-                 std::string* err) {
+                 std::string* err, const std::vector<uint8_t>* kept) {
     const uint32_t np = tree->n_patterns, nn = tree->n_nodes;
     if ((np && !tree->patterns) || (nn && !tree->nodes)) return AUTHJX_EINVAL;
     for (int32_t rt : roots)
@@ -808,6 +810,11 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                     any = true;
                 }
                 if (all && k) eg[sidx].pad[0] = kEagerAll;
+                // a selector of a root-less forest tree: its record is written even when its
+                // patterns were decided in the scan (authjx_select_from_eval_device reads it)
+                bool keep = false;
+                for (uint16_t pi : sel_pats[sidx]) keep = keep || (kept && pi < kept->size() && (*kept)[pi]);
+                if (keep) eg[sidx].pad[0] |= kEagerKeep;
 
             }
             if (any) {

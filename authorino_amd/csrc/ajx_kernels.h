@@ -53,6 +53,24 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false,
                             bool keep_rows = true);
 
+// The lean single-pass kernel (ajx_lean.hip, one ruleset for the batch): stage A with the
+// lean scan and stage B per work-item; requests it can not prove go to d_slow_ids (the
+// caller zeroes d_slow_count first and runs the exact scan after). shared_blob_bytes: the
+// blob of sets[0] is staged into LDS (0: read from global memory). abl (profiling builds
+// with AJX_LEAN_ABLATIONS, kernel modes 15..18): 1..4 the stage-A ablations, no stage B.
+hipError_t launch_lean(const uint8_t* const* d_sets, uint32_t shared_blob_bytes, const uint8_t* d_arena,
+                       const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint64_t* d_rows,
+                       uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, uint8_t* d_tri,
+                       int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream, int abl,
+                       const uint32_t* d_perm, bool keep_rows);
+
+// The multi-tenant single-pass kernel (ajx_lean.hip): each workgroup stages its runs'
+// rulesets in LDS; waves of one staged ruleset run the lean scan, others the token scanner.
+hipError_t launch_tenant(const uint8_t* const* d_sets, const uint32_t* d_set_of_req, const uint8_t* d_arena,
+                         const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint64_t* d_rows,
+                         uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, uint8_t* d_tri,
+                         int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream, const uint32_t* d_perm);
+
 // The streaming kernel (ajx_stream.h), its stage B (ajx_stream_finish) and the exact scan of
 // what they hand over: one ruleset for the batch (sets[0], staged in LDS); stream_eligible
 // says whether it can take the ruleset. d_rows: rows of row_stride >= 5 + n_rec

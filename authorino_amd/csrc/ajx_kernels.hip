@@ -14,27 +14,13 @@
 #include <atomic>
 
 #include "ajx_fast.h"
-#include "ajx_lean.h"
 #include "ajx_modifiers.h"
 #include "ajx_stream.h"
 #include "ajx_kernels.h"
+#include "ajx_kcommon.h"
 
 namespace ajx {
 
-// The dynamic-LDS ceiling of a group of kernels is set once per device (the attribute
-// belongs to that device's code object); any thread may launch first, so the per-device
-// bits are atomic (setting an attribute twice is harmless).
-template <class F>
-static hipError_t attr_once(std::atomic<uint64_t>& done, F set) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    const uint64_t bit = dev >= 0 && dev < 64 ? 1ull << dev : 0ull;
-    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
-    if ((e = set()) != hipSuccess) return e;
-    done.fetch_or(bit, std::memory_order_acq_rel);
-    return hipSuccess;
-}
 
 constexpr int kSelCache = 32;  // resolved selector values kept per request
 constexpr int kPatCache = 64;  // pattern results kept per request for the fold
@@ -183,163 +169,8 @@ static void launch_slow_list(bool mods, uint32_t sgrid, hipStream_t stream, cons
                            d_offs, d_lens, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride);
 }
 
-// SHARED kernels: the whole batch uses sets[0], and the ruleset blob (trie, key table,
-// patterns, literals, DFA tables, fold code — h->total_bytes, a multiple of 16) is
-// copied into dynamic LDS once per workgroup; every thread reaches the barrier. All
-// table reads of the scan and the patterns are then ds_reads.
-// copies nq 16-byte words, four loads in flight per thread before their stores. The source
-// is read as global memory (a blob pointer loaded from the set table is generic: flat
-// loads otherwise), every load unconditional (a clamped index past the end), so that
-// nothing goes to scratch.
-__device__ __forceinline__ void copy_words(uint4* __restrict__ dst, const uint4* __restrict__ src, uint32_t nq,
-                                           uint32_t t, uint32_t nt) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const __attribute__((address_space(1))) uint4* g = (const __attribute__((address_space(1))) uint4*)src;
-#else
-    const uint4* g = src;  // (host pass of the kernel source: never run)
-#endif
-    const uint32_t last = nq - 1u;
-    for (uint32_t b = t; b < nq; b += 4u * nt) {
-        const uint32_t k1 = b + nt, k2 = b + 2u * nt, k3 = b + 3u * nt;
-        const uint4 v0 = g[b];
-        const uint4 v1 = g[k1 < nq ? k1 : last];
-        const uint4 v2 = g[k2 < nq ? k2 : last];
-        const uint4 v3 = g[k3 < nq ? k3 : last];
-        dst[b] = v0;
-        if (k1 < nq) dst[k1] = v1;
-        if (k2 < nq) dst[k2] = v2;
-        if (k3 < nq) dst[k3] = v3;
-    }
-}
 
-// copy_words with every load unconditional (past the end, word b again): the array stays
-// in registers (the streaming kernel's per-wave blob copy: c4 serving 7.8 k -> 4.0 k clocks)
-__device__ __forceinline__ void copy_words_reg(uint4* __restrict__ dst, const uint4* __restrict__ src, uint32_t nq,
-                                               uint32_t t, uint32_t nt) {
-    for (uint32_t b = t; b < nq; b += 8u * nt) {
-        uint4 v[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) {
-            const uint32_t k = b + j * nt;
-            v[j] = src[k < nq ? k : b];
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++)
-            if (b + j * nt < nq) dst[b + j * nt] = v[j];
-    }
-}
 
-template <bool SHARED>
-__device__ __forceinline__ const uint8_t* stage_blob(const uint8_t* gblob) {
-    if constexpr (SHARED) {
-        extern __shared__ uint4 s_blob[];
-        const uint32_t nq = reinterpret_cast<const RulesetHdr*>(gblob)->total_bytes / 16;
-        copy_words(s_blob, reinterpret_cast<const uint4*>(gblob), nq, threadIdx.x, blockDim.x);
-        __syncthreads();
-        return reinterpret_cast<const uint8_t*>(s_blob);
-    } else {
-        return gblob;
-    }
-}
-
-// the work-item's 128-B window ring in dynamic LDS: [blob copy (SHARED)] [ring: per wave
-// 8 chunks x 64 lanes x 16 B]
-constexpr uint32_t kWinRingBytesPerWave = 8 * 64 * 16;
-// single-pass workgroups of 4, 8 or 16 waves (fast_block): one LDS copy of the ruleset
-// blob per workgroup next to its waves' rings, so 16 waves per CU fit the 160 KiB for
-// blobs up to ~8 KiB in 4-wave groups, ~16 KiB in 8-wave groups, ~32 KiB in one 16-wave
-// group (4 waves/SIMD by registers either way)
-constexpr uint32_t kFastBlock = 512;
-constexpr uint32_t kFastMaxBlock = 1024;
-#ifndef AJX_FAST_WAVES
-#define AJX_FAST_WAVES 4  // waves per SIMD the single-pass kernels' register budget is set for
-#endif
-// the workgroup size that fits the most waves per CU for a staged blob of `blob_bytes`
-// (0: nothing staged); the smallest such size on a tie: a workgroup retires as a unit, so
-// smaller ones leave fewer idle waves behind the longest document (measured: c2 4-wave
-// 2.03 ms vs 8-wave 2.11; c3 at 16 waves/CU 2 x 8-wave 3.78 vs 1 x 16-wave 4.03)
-static uint32_t fast_block(uint32_t blob_bytes) {
-    const uint32_t stage = (blob_bytes + 15u) & ~15u;
-    uint32_t best = 0, best_w = 0;
-    for (uint32_t b = 256; b <= kFastMaxBlock; b *= 2) {
-        const uint32_t lds = stage + (b / 64) * kWinRingBytesPerWave;
-        uint32_t w = lds <= 160u * 1024u ? (160u * 1024u / lds) * (b / 64) : 0u;
-        if (w > 4u * AJX_FAST_WAVES) w = 4u * AJX_FAST_WAVES;
-        if (w > best_w) best = b, best_w = w;
-    }
-    return best ? best : 256u;
-}
-__device__ __forceinline__ WinRing lane_ring(uint32_t ring_off) {
-    extern __shared__ uint4 s_dyn_ring[];
-    WinRing r;
-    r.base = reinterpret_cast<uint8_t*>(s_dyn_ring) + ring_off + (threadIdx.x >> 6) * kWinRingBytesPerWave;
-    r.lane16 = (threadIdx.x & 63u) * 16u;
-    r.cstride = 64u * 16u;
-    return r;
-}
-
-// stage A for request r: single-pass scan into its capture row (false: slow list)
-template <int MODE>
-__device__ __forceinline__ bool scan_request(const uint8_t* blob, const uint8_t* d, uint32_t len, RowRef row,
-                                             const WinRing& ring) {
-    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    if (!(h->flags & kFlagFastOk) || len >= (1u << 24)) {
-        row[0] = kRowSlow;
-        return false;
-    }
-    const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-    auto load = [&](uint32_t b, uint32_t nblk) -> Block16 {
-        if (b < nblk) {
-            const uint4 v = a4[b];
-            return Block16{v.x, v.y, v.z, v.w};
-        }
-        return Block16{0u, 0u, 0u, 0u};
-    };
-    return scan_doc<MODE>(blob, blob_tables(blob), d, len, row, ring, load);
-}
-
-// the And/Or fold of every tree of the ruleset on the pattern bitmaps; a forest ruleset
-// (authjx_compile_forest) writes its n_trees results at r * n_trees + k
-__device__ __forceinline__ void fold_outputs(uint32_t r, const uint8_t* blob, const RulesetHdr* h, const uint64_t t[2],
-                                             const uint64_t u[2], const uint64_t se[2],
-                                             uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err) {
-    const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
-    const uint32_t nt = h->pad1[0];
-    if (nt == 0) {
-        int32_t ep;
-        out_tri[r] = run_fold_bits(code, h->n_code, t, u, se, &ep);
-        if (out_err) out_err[r] = ep;
-        return;
-    }
-    const uint32_t* rc = reinterpret_cast<const uint32_t*>(blob + h->pad1[1]);
-    for (uint32_t k = 0; k < nt; k++) {
-        int32_t ep;
-        out_tri[(size_t)r * nt + k] = run_fold_bits(code + rc[2 * k], rc[2 * k + 1], t, u, se, &ep);
-        if (out_err) out_err[(size_t)r * nt + k] = ep;
-    }
-}
-
-// stage B for request r on its capture row: patterns, T bitmap, And/Or fold, outputs.
-// false (nothing written): a value needs the exact scan (a number only ajx_float.h
-// decides), the caller hands the request over
-__device__ __forceinline__ bool finish_request(uint32_t r, const uint8_t* blob, const uint8_t* d, RowRef row,
-                                               uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-                                               uint64_t* __restrict__ out_bm, uint32_t stride,
-                                               const uint64_t* dec = nullptr) {
-    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    uint64_t t[2], u[2];
-    patterns_from_row(blob, d, row, t, u, dec);
-    if ((u[0] & ~h->unsupported[0]) | (u[1] & ~h->unsupported[1])) return false;
-    if (out_bm) {
-        uint64_t* orow = out_bm + (size_t)r * stride;
-        orow[0] = t[0];
-        if (stride > 1) orow[1] = t[1];
-        for (uint32_t w = 2; w < stride; w++) orow[w] = 0ull;
-    }
-    const uint64_t se[2] = {h->static_error[0], h->static_error[1]};
-    fold_outputs(r, blob, h, t, u, se, out_tri, out_err);
-    return true;
-}
 
 // Stage A alone (profiling split / ablations): structural scan -> capture rows.
 // MODE 1/2 are the loads-only / loads+classification ablations.
@@ -410,186 +241,7 @@ __global__ __launch_bounds__(kFastMaxBlock, AJX_FAST_WAVES) void ajx_scan_fused(
     }
 }
 
-// The lean single-pass kernel (ajx_lean.h): stage A with the lean scan, then stage B in the
-// same work-item. Dynamic LDS: [blob copy (SHARED)] [per wave: 64 lanes x 144-B rings].
-constexpr uint32_t kLeanRingBytesPerWave = 64 * lean::kRingStride;
-#ifndef AJX_LEAN_WAVES
-#define AJX_LEAN_WAVES AJX_FAST_WAVES  // waves per SIMD the lean kernel's registers are set for
-#endif
-#ifndef AJX_LEAN_MAXBLOCK
-#define AJX_LEAN_MAXBLOCK kFastMaxBlock
-#endif
-// ABL: profiling ablations (kernel modes 15..18, lean::scan_doc): stage A cut short, no stage B
-template <bool SHARED, int ABL = 0>
-__global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_lean(
-    const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
-    uint64_t* __restrict__ rows, uint32_t row_stride, uint32_t* __restrict__ slow_count,
-    uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-    uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t ring_off, const uint32_t* __restrict__ perm,
-    uint32_t keep_rows) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t r = k < n ? (perm ? perm[k] : k) : 0u;
-    const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : set_of_req[r]]);
-    if (k >= n) return;
-    extern __shared__ uint4 s_lean_dyn[];
-    uint8_t* ring = reinterpret_cast<uint8_t*>(s_lean_dyn) + ring_off + threadIdx.x * lean::kRingStride;
-    const RowRef row = wave_row(rows, row_stride, k);
-    const uint8_t* d = arena + offs[r];
-    const uint32_t len = lens[r];
-    const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-    bool ok = (h->flags & kFlagFastOk) && len < (1u << 24);
-    uint64_t dec[2] = {0ull, 0ull};
-    if (ok) {
-        const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-        auto load = [&](uint32_t b, uint32_t nblk) -> Block16 {
-            if (b < nblk) {
-                const uint4 v = a4[b];
-                return Block16{v.x, v.y, v.z, v.w};
-            }
-            return Block16{0u, 0u, 0u, 0u};
-        };
-        ok = lean::scan_doc<ABL>(blob, blob_tables(blob), d, len, row, ring, threadIdx.x & 63u, load, dec,
-                                 keep_rows);
-    } else {
-        row[0] = kRowSlow;
-    }
-    if constexpr (ABL != 0) {
-        if (dec[0] ^ dec[1]) row[0] ^= dec[0] ^ dec[1];
-        return;
-    }
-    if (!ok) {
-        slow_ids[atomicAdd(slow_count, 1u)] = r;
-        return;
-    }
-    if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec)) {
-        row[0] = kRowSlow;
-        slow_ids[atomicAdd(slow_count, 1u)] = r;
-    }
-}
-// workgroup size for the lean kernel with a staged blob of `blob_bytes` (as fast_block)
-static uint32_t lean_block(uint32_t blob_bytes) {
-    const uint32_t stage = (blob_bytes + 15u) & ~15u;
-    uint32_t best = 0, best_w = 0;
-    for (uint32_t b = 256; b <= AJX_LEAN_MAXBLOCK; b *= 2) {
-        const uint32_t lds = stage + (b / 64) * kLeanRingBytesPerWave;
-        uint32_t w = lds <= 160u * 1024u ? (160u * 1024u / lds) * (b / 64) : 0u;
-        if (w > 4u * AJX_LEAN_WAVES) w = 4u * AJX_LEAN_WAVES;
-        if (w > best_w) best = b, best_w = w;
-    }
-    return best ? best : 256u;
-}
 
-// The single-pass kernel for multi-tenant batches (one ruleset per request through
-// set_of_req; the caller buckets requests by AuthConfig, so a workgroup's requests form a
-// few runs of one ruleset each). The workgroup finds its runs (a run starts where the
-// ruleset differs from the previous work-item's) and copies the blobs of its first runs
-// into LDS — each blob's hot prefix, [0, hot_bytes), which holds every table this kernel
-// reads — as many as fit the staging region; a wave whose requests all fall in staged
-// runs reads every table from LDS (each lane from its own run's copy), any other wave
-// reads them from global memory. Dynamic LDS: [staging region (ring_off bytes)] [rings].
-constexpr uint32_t kTenantRuns = 8;  // runs a workgroup may stage
-static_assert(kLeanRingBytesPerWave == kWinRingBytesPerWave, "the tenant kernel's rings serve both scans");
-__global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_tenant(
-    const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
-    const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
-    uint64_t* __restrict__ rows, uint32_t row_stride, uint32_t* __restrict__ slow_count,
-    uint32_t* __restrict__ slow_ids, uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
-    uint64_t* __restrict__ out_bm, uint32_t stride, uint32_t ring_off, const uint32_t* __restrict__ perm) {
-    extern __shared__ uint4 s_stage[];
-    __shared__ uint32_t s_wcnt[kFastBlock / 64];
-    __shared__ uint32_t s_rsid[kTenantRuns];
-    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, nw = blockDim.x >> 6;
-    const uint32_t k = blockIdx.x * blockDim.x + t;  // (the grid covers n: n > 0 here)
-    const uint32_t kc = k < n ? k : n - 1u;           // (tail threads: the last request's run)
-    const uint32_t r = perm ? perm[kc] : kc;
-    const uint32_t sid = set_of_req[r];
-    bool start = t == 0;
-    if (!start) {
-        const uint32_t kp = (k - 1u) < n ? k - 1u : n - 1u;
-        start = set_of_req[perm ? perm[kp] : kp] != sid;
-    }
-    // run index of every work-item: starts before it in the workgroup, minus one
-    const uint64_t m = __ballot(start);
-    if (lane == 0) s_wcnt[wv] = (uint32_t)__builtin_popcountll(m);
-    __syncthreads();
-    uint32_t base = 0, nrun = 0;
-    for (uint32_t i = 0; i < nw; i++) {
-        const uint32_t c = s_wcnt[i];
-        base += i < wv ? c : 0u;
-        nrun += c;
-    }
-    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-    const uint32_t ridx = base + (uint32_t)__builtin_popcountll(m & upto) - 1u;
-    if (start && ridx < kTenantRuns) s_rsid[ridx] = sid;
-    __syncthreads();
-    // stage the leading runs' blobs while they fit (every thread walks the same list)
-    uint32_t nst = 0, off = 0, my_off = 0;
-    const uint32_t nr = nrun < kTenantRuns ? nrun : kTenantRuns;
-    for (uint32_t j = 0; j < nr; j++) {
-        const uint8_t* g = sets[s_rsid[j]];
-        const uint32_t bytes = reinterpret_cast<const RulesetHdr*>(g)->hot_bytes;  // (a multiple of 16)
-        if (off + bytes > ring_off) break;
-        const uint4* src = reinterpret_cast<const uint4*>(g);
-        for (uint32_t i = t; i < bytes / 16u; i += blockDim.x) s_stage[off / 16u + i] = src[i];
-        if (j == ridx) my_off = off;
-        off += bytes;
-        nst++;
-    }
-    __syncthreads();
-    const RowRef row = wave_row(rows, row_stride, k);
-    const uint8_t* d = arena + offs[r];
-    // (wave-uniform: the whole wave takes the LDS tables or the global ones)
-    if (__all(ridx < nst)) {
-        // a wave whose requests all use one staged ruleset (the caller's bucketing makes most
-        // waves so: 84 % of c4's) runs the lean scan on that copy (ajx_scan_lean's
-        // per-request body); a wave of several rulesets, the token scanner with each lane's
-        // own copy. (As two kernels, one per kind of wave, each with its own registers: c4
-        // 5.57 ms against 4.85 ms for this one.)
-        const uint32_t off0 = lean::uni(my_off);
-        if (__all(my_off == off0)) {
-            const uint8_t* blob = reinterpret_cast<const uint8_t*>(s_stage) + off0;
-            if (k >= n) return;
-            const uint32_t len = lens[r];
-            const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
-            uint64_t dec[2] = {0ull, 0ull};
-            bool ok = (h->flags & kFlagFastOk) && len < (1u << 24);
-            if (ok) {
-                uint8_t* ring = reinterpret_cast<uint8_t*>(s_stage) + ring_off + t * lean::kRingStride;
-                const uint4* a4 = reinterpret_cast<const uint4*>(d - ((uintptr_t)d & 15u));
-                auto load = [&](uint32_t b, uint32_t nblk) -> Block16 {
-                    if (b < nblk) {
-                        const uint4 v = a4[b];
-                        return Block16{v.x, v.y, v.z, v.w};
-                    }
-                    return Block16{0u, 0u, 0u, 0u};
-                };
-                ok = lean::scan_doc(blob, blob_tables(blob), d, len, row, ring, lane, load, dec, 0u) &&
-                     finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec);
-            }
-            if (!ok) {
-                row[0] = kRowSlow;
-                slow_ids[atomicAdd(slow_count, 1u)] = r;
-            }
-            return;
-        }
-        const uint8_t* blob = reinterpret_cast<const uint8_t*>(s_stage) + my_off;
-        if (k >= n) return;
-        if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off)) ||
-            !finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
-            row[0] = kRowSlow;
-            slow_ids[atomicAdd(slow_count, 1u)] = r;
-        }
-    } else {
-        const uint8_t* gblob = sets[sid];
-        if (k >= n) return;
-        if (!scan_request<0>(gblob, d, lens[r], row, lane_ring(ring_off)) ||
-            !finish_request(r, gblob, d, row, out_tri, out_err, out_bm, stride)) {
-            row[0] = kRowSlow;
-            slow_ids[atomicAdd(slow_count, 1u)] = r;
-        }
-    }
-}
 
 // a stage-B list entry the stream could not prove (merge_slow): the exact scan decides it
 constexpr uint32_t kStageExact = 1u << 31;
@@ -1282,22 +934,9 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             reinterpret_cast<const void*>(&ajx_scan_fast<0, false>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<1, true>),
                             reinterpret_cast<const void*>(&ajx_scan_fast<2, true>),
-                            reinterpret_cast<const void*>(&ajx_scan_fused),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<true>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<false>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 1>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 2>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 3>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 4>)};
+                            reinterpret_cast<const void*>(&ajx_scan_fused)};
         for (const void* k : ks) {
             const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (r != hipSuccess) return r;
-        }
-        // (the tenant kernel also holds static LDS for __syncthreads_and: ask only for what
-        // its launch uses, blob + four window rings)
-        for (const void* k : {reinterpret_cast<const void*>(&ajx_scan_fused_tenant)}) {
-            const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     kMaxTenantStageBytes + 4 * kWinRingBytesPerWave);
             if (r != hipSuccess) return r;
         }
         return hipSuccess;
@@ -1327,42 +966,25 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
             hipLaunchKernelGGL((ajx_patterns<false>), dim3(grid), dim3(block), 0, stream, d_sets, d_set_of_req,
                                d_arena, d_offs, n, d_rows, row_stride, d_tri, d_err, d_bm, stride);
         }
-    } else if (mode >= 15 && mode <= 18) {  // profiling: lean stage-A ablations (one staged ruleset)
-        if (!shared) return hipErrorInvalidValue;
-        const uint32_t lblock = lean_block(shared_blob_bytes), lgrid = (n + lblock - 1) / lblock;
-        const uint32_t llds = ring_off + (lblock / 64) * kLeanRingBytesPerWave;
-        auto k = mode == 15 ? &ajx_scan_lean<true, 1> : mode == 16 ? &ajx_scan_lean<true, 2>
-               : mode == 17 ? &ajx_scan_lean<true, 3> : &ajx_scan_lean<true, 4>;
-        hipLaunchKernelGGL(k, dim3(lgrid), dim3(lblock), llds, stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, n,
-                           d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, ring_off, d_perm,
-                           keep_rows ? 1u : 0u);
-        return hipGetLastError();
-    } else if (!d_set_of_req) {  // the lean single-pass kernel (one ruleset)
+    } else if ((mode >= 15 && mode <= 18) || !d_set_of_req) {
+        // the lean single-pass kernel (one ruleset; ajx_lean.hip), or its profiling ablations
         // (multi-tenant batches: the staged tenant scanner below. Measured on c4, the lean
         // scan with per-lane table parameters took 6.39 ms and one pass per ruleset of a
         // wave 7.3-7.8 ms, against 5.38 ms for the tenant kernel's LDS-staged tables)
-        const uint32_t lblock = shared ? lean_block(shared_blob_bytes) : 256u;
-        const uint32_t lgrid = (n + lblock - 1) / lblock;
-        const uint32_t llds = ring_off + (lblock / 64) * kLeanRingBytesPerWave;
-        if (shared)
-            hipLaunchKernelGGL((ajx_scan_lean<true>), dim3(lgrid), dim3(lblock), llds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
-                               d_bm, stride, ring_off, d_perm, keep_rows ? 1u : 0u);
-        else
-            hipLaunchKernelGGL((ajx_scan_lean<false>), dim3(lgrid), dim3(lblock), llds, stream, d_sets, d_set_of_req,
-                               d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err,
-                               d_bm, stride, ring_off, d_perm, keep_rows ? 1u : 0u);
+        if (mode >= 15 && !shared) return hipErrorInvalidValue;
+        e = launch_lean(d_sets, shared ? shared_blob_bytes : 0u, d_arena, d_offs, d_lens, n, d_rows, row_stride,
+                        d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, stream, mode >= 15 ? mode - 14 : 0,
+                        d_perm, keep_rows);
+        if (e != hipSuccess || mode >= 15) return e;
     } else if (shared_blob_bytes) {
         // multi-tenant batch (shared_blob_bytes != 0: staging on): each workgroup stages its
         // runs' rulesets, those that fit (ajx_scan_fused_tenant);
         // 4-wave workgroups, so more of them fall inside one AuthConfig's bucket
         // (staging region: the tenant budget less room for the kernel's static LDS, so
         // four groups still fit a CU)
-        const uint32_t tblock = 256, tgrid = (n + tblock - 1) / tblock;
-        const uint32_t toff = kMaxTenantStageBytes - 256u;
-        hipLaunchKernelGGL(ajx_scan_fused_tenant, dim3(tgrid), dim3(tblock), toff + (tblock / 64) * kWinRingBytesPerWave,
-                           stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count,
-                           d_slow_ids, d_tri, d_err, d_bm, stride, toff, d_perm);
+        e = launch_tenant(d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count,
+                          d_slow_ids, d_tri, d_err, d_bm, stride, stream, d_perm);
+        if (e != hipSuccess) return e;
     } else {
         hipLaunchKernelGGL(ajx_scan_fused, dim3(grid), dim3(block), lds, stream, d_sets, d_set_of_req,
                            d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm,

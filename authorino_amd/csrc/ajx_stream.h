@@ -40,7 +40,7 @@
 // After the span, each lane runs stage B (ajx_fast.h patterns_from_row) for one document
 // of the span on its LDS capture row.
 #pragma once
-#include "ajx_lean.h"
+#include "ajx_lean_cls.h"
 #include "ajx_wave.h"
 
 namespace ajx {

@@ -238,8 +238,11 @@ int authjx_select_batch_device(authjx_ctx* ctx, const authjx_ruleset* const* set
  * default kernel keeps capture rows for forests only). For a phase compiled with authjx_compile_forest whose
  * last tree holds the response selectors (AUTHJX_OP_EQ patterns, root -1), this resolves
  * them without a second document scan: the gjson.Get of JSONValue.ResolveFor
- * (pkg/json/json.go:41-53) after the rules of the same request. AUTHJX_EINVAL when the
- * rows are not that evaluation's. Asynchronous on `stream`; order it after the eval. */
+ * (pkg/json/json.go:41-53) after the rules of the same request. The patterns must belong
+ * to root-less trees of the forest (the kernel writes capture records only for those and
+ * for the values its stage B reads). AUTHJX_EINVAL when the rows are not that
+ * evaluation's, or a pattern's record is not kept. Asynchronous on `stream`; order it
+ * after the eval. */
 int authjx_select_from_eval_device(authjx_ctx* ctx, const authjx_ruleset* rs, uint32_t first_pattern,
                                    const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens,
                                    uint32_t n, authjx_value* d_out_values, uint32_t values_stride, void* stream);

@@ -91,6 +91,37 @@ class HostRuleset:
         self.error = err.value.decode()
 
     @classmethod
+    def forest(cls, trees):
+        """trees: [(patterns, nodes, root)] compiled as one forest ruleset (ht_compile_forest;
+        root -1: a root-less tree, whose selectors' capture records the kernel keeps)."""
+        self = cls.__new__(cls)
+        built = [make_tree(*t) for t in trees]
+        self._keep = [k for _, k in built]
+        arr = (_Tree * len(trees))(*[t for t, _ in built])
+        self._keep.append(arr)
+        self.n = sum(len(t[0]) for t in trees)
+        err = C.create_string_buffer(512)
+        rc = C.c_int(0)
+        L = lib()
+        L.ht_compile_forest.argtypes = [C.POINTER(_Tree), C.c_uint32, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
+        L.ht_compile_forest.restype = C.c_void_p
+        self._h = L.ht_compile_forest(arr, len(trees), err, 512, C.byref(rc))
+        self.rc = rc.value
+        self.status = []
+        self.error = err.value.decode()
+        return self
+
+    @classmethod
+    def with_selector_tree(cls, expr):
+        """expr's tree plus a root-less tree of an EQ "" pattern per selector (the response
+        selectors' shape, runtime.Context.compile_forest(extra_selectors=...)): every
+        selector's capture record is kept."""
+        pats, nodes, root = expr.flatten()
+        sels = list(dict.fromkeys(p.selector for p in pats))
+        return cls.forest([([(p.selector, int(p.operator), p.value) for p in pats], nodes, root),
+                           ([(s, 1, "") for s in sels], [], -1)])
+
+    @classmethod
     def from_expression(cls, expr):
         pats, nodes, root = expr.flatten()
         return cls([(p.selector, int(p.operator), p.value) for p in pats], nodes, root)
@@ -206,7 +237,8 @@ def _lean_decl():
 
 def lean_keep(keep: bool) -> None:
     """keep False: the lean scan writes only the capture records stage B needs (the
-    kernel's default when no caller reads the rows); True: every record."""
+    kernel's default when no caller reads the rows); True: also those of the selectors a
+    caller reads back (a forest's root-less trees, kEagerKeep)."""
     L = lib()
     L.ht_lean_keep.argtypes = [C.c_int]
     L.ht_lean_keep(1 if keep else 0)

@@ -33,6 +33,16 @@ void* ht_compile(const authjx_tree* tree, int32_t* status, char* err, size_t cap
     return r;
 }
 
+// a forest (authjx_compile_forest): trees[n], one fold program each
+void* ht_compile_forest(const authjx_tree* trees, uint32_t n, char* err, size_t cap, int* rc) {
+    HtRuleset* r = new HtRuleset();
+    std::string e;
+    *rc = compile_forest(trees, n, &r->c, &e);
+    if (err && cap) std::snprintf(err, cap, "%s", e.c_str());
+    if (*rc != AUTHJX_OK) { delete r; return nullptr; }
+    return r;
+}
+
 void ht_free(void* h) { delete (HtRuleset*)h; }
 
 // evaluate one document; res[p] receives each pattern's tri-state
@@ -271,6 +281,7 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
     const RulesetHdr* hd = (const RulesetHdr*)blob;
     if (!(hd->flags & kFlagFastOk)) return -2;
+    if (len == 0) return -1;  // (the kernels send empty documents to the exact scan)
     std::vector<uint8_t> buf(len + 96, 0x7A);  // (neighbour bytes around the document)
     uintptr_t base = ((uintptr_t)buf.data() + 15) & ~(uintptr_t)15;
     uint8_t* d = (uint8_t*)base + (mis & 15);
@@ -278,15 +289,13 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
     std::vector<uint64_t> row(1 + hd->n_selectors, 0xDEADBEEFDEADBEEFull);
     const uint32_t* a = (const uint32_t*)(d - (mis & 15));
     const uint32_t nb = (uint32_t)((buf.data() + buf.size() - (const uint8_t*)a) / 16);
-    alignas(16) uint8_t ring_mem[lean::kRingStride];
-    std::memset(ring_mem, 0x5A, sizeof ring_mem);
-    auto load = [&](uint32_t b, uint32_t nblk) -> Block16 {
-        if (b < nblk && b < nb) return Block16{a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
-        return Block16{0, 0, 0, 0};
-    };
+    // the wave's ring (chunk-major); this document's lane: mis * 5 (every lane offset used)
+    static thread_local std::vector<uint8_t> ring_mem(lean::kRingBytesPerWave);
+    std::memset(ring_mem.data(), 0x5A, ring_mem.size());
+    const uint32_t nblk = (len + (mis & 15) + 15) / 16;
+    lean::CopyLoader ld{(const uint8_t*)a, nblk, nb, ring_mem.data() + ((mis * 5u) & 63u) * 16u};
     uint64_t dec[2] = {0, 0};
-    const bool ok =
-        lean::scan_doc(blob, blob_tables(blob), d, len, row.data(), ring_mem, (uint32_t)mis * 5u, load, dec, g_lean_keep);
+    const bool ok = lean::scan_doc(blob, len, (uint32_t)(mis & 15), row.data(), ld.lane_ring, ld, dec, g_lean_keep);
     g_last_dec[0] = dec[0];
     g_last_dec[1] = dec[1];
     if (!ok) return -1;

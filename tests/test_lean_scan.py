@@ -48,8 +48,9 @@ def _chain(n):
 
 @pytest.fixture(params=[True, False], ids=["keep_rows", "needed_rows"])
 def keep(request):
-    """Both capture-row modes of the lean scan: every record (a caller reads the rows) and
-    only what stage B needs (values decided in the scan leave no record)."""
+    """Both capture-row modes of the lean scan: rows a caller reads (the records of its
+    selectors, kEagerKeep, as well) and only what stage B needs (values decided in the scan
+    leave no record)."""
     H.lean_keep(request.param)
     yield request.param
     H.lean_keep(True)
@@ -87,8 +88,11 @@ def test_lean_decides_workload_documents(workload, keep):
     from authorino_amd import workloads as W
 
     w = W.make(workload, n=300, seed=17)
-    hr = H.HostRuleset.from_expression(w.expr)
+    # kept rows: the forest with a root-less tree of every selector (what a caller of
+    # authjx_select_from_eval_device compiles): every record is written
+    hr = H.HostRuleset.with_selector_tree(w.expr) if keep else H.HostRuleset.from_expression(w.expr)
     rs = O.Ruleset.from_expression(w.expr)
+    np_ = len(w.expr.flatten()[0])
     n_sel = len({p.selector for p in w.expr.flatten()[0]})
     for i in range(w.n):
         d = w.doc(i)
@@ -100,8 +104,10 @@ def test_lean_decides_workload_documents(workload, keep):
             if keep:
                 assert lrow == trow, (i, d)
             assert lres == tres and tl == tt and el == et
-            t_or, _ = rs.matches(d)
-            assert tl == t_or
+            assert lres[:np_] == [rs.pattern(p, d) for p in range(np_)]
+            if not keep:
+                t_or, _ = rs.matches(d)
+                assert tl == t_or
 
 
 def _tree(rng, depth, keys):
@@ -161,8 +167,10 @@ def test_lean_deep_trees_selectors_from_the_document(seed):
         ot = [rs.pattern(p, d) for p in range(len(pats))]
         if O.UNSUPPORTED in ot:
             continue
-        hr = H.HostRuleset(pats, nodes, root)
-        n_sel = len({p[0] for p in pats})
+        # (with a root-less tree of every selector: rows a caller reads, every record kept)
+        sels = list(dict.fromkeys(p[0] for p in pats))
+        hr = H.HostRuleset.forest([(pats, nodes, root), ([(x, 1, "") for x in sels], [], -1)])
+        n_sel = len(sels)
         for mis in (0, int(rng.integers(1, 16))):
             total += 1
             tl, _, lres, lrow = H.eval_lean(hr, d, mis=mis, n_sel=n_sel)
@@ -170,7 +178,7 @@ def test_lean_deep_trees_selectors_from_the_document(seed):
             decided_tok += tt >= 0
             if tl >= 0:
                 decided += 1
-                assert lres == ot, (pats, d)
+                assert lres[:len(pats)] == ot, (pats, d)
                 if tt >= 0:
                     assert lrow == trow, (pats, d, mis)
     # (selectors into containers nested in indexed arrays, deep index chains: the exact
