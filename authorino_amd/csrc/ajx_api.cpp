@@ -609,7 +609,7 @@ static int eval_device(authjx_ctx* ctx, const authjx_ruleset* const* sets, uint3
         HIP_OK(ajx::launch_eval_fast(w->d_sets, d_set_of_req, stage_bytes, d_arena, d_offs, d_lens, n,
                                      d_out_tristate, d_out_err_idx, d_out_bitmap, bitmap_stride_words,
                                      w->d_rows, row_stride, w->d_slow, w->d_slow + 1, s,
-                                     ablate < 20 ? ablate : 0, perm, mods, keep_rows));
+                                     ablate < 20 ? ablate : 0, perm, mods, keep_rows, n_sets == 1 ? h0->lean_feat : 3u));
     }
     return batch_done(w, sets, n_sets);
 }
@@ -1033,9 +1033,10 @@ int authjx_batcher_create(authjx_ctx* ctx, uint32_t max_batch, uint32_t window_u
 }
 
 // Profiling only (not in authjx.h): worker threads (each with its own stream) of the
-// batchers created after this call (1..8; default 2)
+// batchers created after this call (1..8; default 2). n = 0 returns the current count.
 int authjx_debug_batcher_workers(uint32_t n) {
-    if (n == 0 || n > kBatcherMaxWorkers) return AUTHJX_EINVAL;
+    if (n == 0) return (int)g_batcher_workers.load();
+    if (n > kBatcherMaxWorkers) return AUTHJX_EINVAL;
     g_batcher_workers.store(n);
     return AUTHJX_OK;
 }

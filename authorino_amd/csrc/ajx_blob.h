@@ -214,12 +214,15 @@ struct RulesetHdr {
     uint32_t key_mult;          // key_slot_hash multiplier
     uint32_t off_eager;         // EagerSel[n_selectors] (0: none)
     uint32_t off_stream;        // StreamHdr (0: the streaming scan can not take this ruleset)
-    uint32_t pad2;
+    uint32_t lean_feat;         // walker features the ruleset needs: kLeanArr | kLeanCaps
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
     uint64_t unsupported[2];    // pattern p can not be decided on the device
 };
 constexpr uint32_t kFlagFastOk = 4;
+// RulesetHdr::lean_feat: some trie node has array-index children (the lean walk enters
+// arrays); some selector's node has children (a captured container is walked into)
+constexpr uint32_t kLeanArr = 1, kLeanCaps = 2;
 
 constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the exact scan's buffers
 

@@ -697,6 +697,11 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         if (nt && i < 128) null_true[i >> 6] |= bit;
     }
     if (fast_ok) flags |= kFlagFastOk;
+    uint32_t lean_feat = 0;
+    for (const TNode& t : trie) {
+        for (const auto& k : t.keys) lean_feat |= k.second >= 0 ? kLeanArr : 0u;
+        if (t.selector >= 0 && !t.kids.empty()) lean_feat |= kLeanCaps;
+    }
 
     // ---- assemble ----
     Builder b;
@@ -1081,6 +1086,7 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     // (KeySlot::key_off8 reaches 512 KiB of literal pool)
     if (lits.size() >= 8u * 65536u) flags &= ~kFlagFastOk;
     hdr.flags = flags;
+    hdr.lean_feat = lean_feat;
     std::memcpy(b.blob.data(), &hdr, sizeof hdr);
     out->blob = std::move(b.blob);
     out->n_patterns = np;

@@ -51,18 +51,19 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
                             int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false,
-                            bool keep_rows = true);
+                            bool keep_rows = true, uint32_t lean_feat = 3);
 
 // The lean single-pass kernel (ajx_lean.hip, one ruleset for the batch): stage A with the
 // lean scan and stage B per work-item; requests it can not prove go to d_slow_ids (the
 // caller zeroes d_slow_count first and runs the exact scan after). shared_blob_bytes: the
 // blob of sets[0] is staged into LDS (0: read from global memory). abl (profiling builds
 // with AJX_LEAN_ABLATIONS, kernel modes 15..18): 1..4 the stage-A ablations, no stage B.
+// lean_feat: RulesetHdr::lean_feat of sets[0] (the walker instance; 3 takes every ruleset).
 hipError_t launch_lean(const uint8_t* const* d_sets, uint32_t shared_blob_bytes, const uint8_t* d_arena,
                        const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint64_t* d_rows,
                        uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, uint8_t* d_tri,
                        int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream, int abl,
-                       const uint32_t* d_perm, bool keep_rows);
+                       const uint32_t* d_perm, bool keep_rows, uint32_t lean_feat);
 
 // The multi-tenant single-pass kernel (ajx_lean.hip): each workgroup stages its runs'
 // rulesets in LDS; waves of one staged ruleset run the lean scan, others the token scanner.

@@ -911,7 +911,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode, const uint32_t* d_perm, bool mods, bool keep_rows) {
+                            int mode, const uint32_t* d_perm, bool mods, bool keep_rows, uint32_t lean_feat) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
     // workgroup size by the waves a CU holds (each workgroup stages its own blob copy)
@@ -974,7 +974,7 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
         if (mode >= 15 && !shared) return hipErrorInvalidValue;
         e = launch_lean(d_sets, shared ? shared_blob_bytes : 0u, d_arena, d_offs, d_lens, n, d_rows, row_stride,
                         d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, stream, mode >= 15 ? mode - 14 : 0,
-                        d_perm, keep_rows);
+                        d_perm, keep_rows, lean_feat);
         if (e != hipSuccess || mode >= 15) return e;
     } else if (shared_blob_bytes) {
         // multi-tenant batch (shared_blob_bytes != 0: staging on): each workgroup stages its

@@ -69,7 +69,13 @@ constexpr uint32_t kIdxKeyLen = kIndexKeyLen;
 
 enum : uint32_t { S_RUN = 0, S_DONE = 1, S_SLOW = 2 };
 
-// The walker of one document.
+// The walker of one document. ARR: the ruleset has array-index selectors (arrays on
+// selector paths are walked element by element; without, every array is squashed: no
+// selector can match inside one); CAPS: a selector's value can be a container the walk
+// enters (a selector that is a prefix of another). The lean kernel takes the instance the
+// ruleset needs (RulesetHdr::lean_feat, kLeanArr / kLeanCaps); the fewer features, the less
+// state and code per iteration.
+template <bool ARR = true, bool CAPS = true>
 struct Walk {
     // tables
     const TrieNode* tn;
@@ -86,6 +92,7 @@ struct Walk {
     uint32_t kinds;         // bit k: container at depth k is an array
     uint64_t nlo, nhi;      // trie node per depth 1..16
     uint32_t top, tarr;     // top container's node, is-array
+    AJX_HD uint32_t ta() const { return ARR ? tarr : 0u; }
     uint32_t expk;          // top object expects a key (1) or its value (0)
     // (the fields the walk touches only at rarer tokens go packed, so the kernel keeps its
     // state in registers without spilling)
@@ -242,7 +249,7 @@ struct Walk {
         return true;
     }
     AJX_HD void close(uint32_t p) {
-        if (ncap) {
+        if (CAPS && ncap) {
             const uint32_t cs = ncap == 2 ? caps >> 16 : caps & 0xFFFFu, start = ncap == 2 ? cap1s : cap0s;
             if ((cs >> 8) == depth) {
                 row[1 + (cs & 0xFFu)] =
@@ -257,9 +264,9 @@ struct Walk {
             return;
         }
         top = node_at(depth);
-        tarr = (kinds >> depth) & 1u;
+        tarr = ARR ? (kinds >> depth) & 1u : 0u;
         expk = 1;
-        if (tarr) {
+        if (ARR && tarr) {
             idx = nasv == 2 ? asv >> 16 : asv & 0xFFFFu;
             nasv--;
         }
@@ -284,13 +291,15 @@ struct Walk {
     AJX_HD void open_f(uint32_t node, uint32_t nf, bool arr, uint32_t p) {
         int32_t s = (int32_t)(int16_t)(nf & 0xFFFFu);
         if (s >= 0 && ((found >> s) & 1)) s = -1;
-        if (node == kNoNode || (nf >> 16 & 0xFFu) == 0) {  // squashed (captured when a leaf)
+        // squashed (captured when a leaf): off every selector path, and arrays whose node
+        // has no array-index children (gjson matches no key inside an array)
+        if (node == kNoNode || (nf >> 16 & 0xFFu) == 0 || (arr && !((nf >> 24) & 1u))) {
             skipw = 1u | ((s >= 0 ? (uint32_t)s + 1u : 0u) << 24);
             skips = p;
             return;
         }
         if (depth + 1 > kMaxLive) { st = S_SLOW; return; }
-        if (tarr) {  // the outer array's element index comes back at its close
+        if (ARR && tarr) {  // the outer array's element index comes back at its close
             if (nasv >= 2 || idx > 0xFFFFu) { st = S_SLOW; return; }
             asv = nasv == 1 ? (asv & 0xFFFFu) | (idx << 16) : nasv == 0 ? (asv & 0xFFFF0000u) | idx : asv;
             nasv++;
@@ -301,12 +310,12 @@ struct Walk {
         const uint64_t lo = nlo, hi = nhi;
         nlo = k < 8 ? (lo & ~m) | x : lo;
         nhi = k < 8 ? hi : (hi & ~m) | x;
-        kinds = arr ? kinds | (1u << depth) : kinds & ~(1u << depth);
+        if (ARR) kinds = arr ? kinds | (1u << depth) : kinds & ~(1u << depth);
         top = node;
-        tarr = arr ? 1u : 0u;
+        tarr = ARR && arr ? 1u : 0u;
         expk = 1;
         idx = 0;
-        if (s >= 0) {
+        if (CAPS && s >= 0) {
             found |= 1ull << s;  // (first match in document order)
             if (ncap >= 2) { st = S_SLOW; return; }
             const uint32_t v = (uint32_t)s | (depth << 8);  // (s < 64, depth <= 16)
@@ -372,12 +381,12 @@ struct Walk {
             {
                 const bool bq = (c.cq >> i) & 1u, bo = (c.op >> i) & 1u, bc = (c.cl >> i) & 1u, kq = (cok >> i) & 1u;
                 const bool root = depth == 0;
-                const bool key = bq && !tarr && expk;  // a key (its closing quote)
-                const bool pv = bq && !tarr && !expk;  // the closing quote of a key's string value
-                const bool el = tarr && !bc;           // an array element (string, container, scalar)
+                const bool key = bq && !ta() && expk;  // a key (its closing quote)
+                const bool pv = bq && !ta() && !expk;  // the closing quote of a key's string value
+                const bool el = ta() && !bc;           // an array element (string, container, scalar)
                 // the grammar the masks can not see: a key where a key belongs, a value where
                 // a value belongs, the root alone at depth 0
-                bad = root ? !(bo && p == 0) : bq ? kq != key : bc ? false : !tarr;
+                bad = root ? !(bo && p == 0) : bq ? kq != key : bc ? false : !ta();
                 // the string's opening quote (a key's, a string element's)
                 const uint32_t oqb = c.oq & below(i);
                 const uint32_t ss = oqb ? cb + hib(oqb) : carry_oq;
@@ -385,7 +394,7 @@ struct Walk {
                 if (key && !bad) bad = klen >= kIdxKeyLen || has_bs(k0, p, c, l);
                 // the key table: a key's (last 8 bytes, length, parent) or an element's index
                 uint32_t node = kNoNode;
-                const bool eidx = el && top != kNoNode && (tn[top].flags & 1);
+                const bool eidx = ARR && el && top != kNoNode && (tn[top].flags & 1);
                 if ((key && !bad) || eidx) {
                     uint64_t sig = r64((p - 8u + mis) & 127u);
                     sig = klen >= 8 ? sig : (klen ? sig >> (8 * (8 - klen)) : 0ull);
@@ -402,7 +411,7 @@ struct Walk {
                 const bool vstr = bq && (!key || vb == '"');
                 const bool vopen = key ? (vb == '{' || vb == '[') : bo;
                 const bool vscal = !bq && !bo && !bc ? true : key && !vstr && !vopen;
-                if (bc) bad |= root || tarr != (vb == ']') || (!tarr && !expk);
+                if (bc) bad |= root || ta() != (vb == ']' ? 1u : 0u) || (!ta() && !expk);
                 // a key's string value: its closing quote from the masks (or pending)
                 uint32_t e = p;
                 bool ended = true;
@@ -494,7 +503,7 @@ struct Walk {
             while (!bad && st == S_RUN && after != kNone) {
                 const uint32_t r = after - cb;
                 if (r >= 64 || !((cl64 >> r) & 1u)) break;
-                bad = depth == 0 || tarr != (rb(after) == ']') || (!tarr && !expk);
+                bad = depth == 0 || ta() != (rb(after) == ']' ? 1u : 0u) || (!ta() && !expk);
                 if (bad) break;
                 if (r < 32) T &= ~(1u << r);
                 else l.tok &= ~(1u << (r - 32));
@@ -527,11 +536,11 @@ struct Walk {
 // longer needs: the next window's first half while the current window's first sub-window
 // is walked (the ring keeps the 32 bytes before that sub-window), its second half while
 // the second one is.
-template <int ABL = 0, class Loader>
+template <int ABL = 0, bool ARR = true, bool CAPS = true, class Loader>
 AJX_HD bool scan_doc(const uint8_t* blob, uint32_t n, uint32_t mis, RowRef row, uint8_t* ring, Loader& ld,
                      uint64_t dec[2], uint32_t keep = 1) {
     const RulesetHdr* h = (const RulesetHdr*)blob;
-    Walk w;
+    Walk<ARR, CAPS> w;
     // the tables as the blob pointer plus uniform offsets: the offsets go to scalar registers
     // and the pointers keep the blob's provenance, so that with the blob staged in LDS every
     // table read is a ds_read (a pointer made uniform through an integer would be generic:

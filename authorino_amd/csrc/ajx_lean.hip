@@ -22,8 +22,9 @@ constexpr uint32_t kLeanMaxBlock = 1024;
 #ifndef AJX_LEAN_MAXBLOCK
 #define AJX_LEAN_MAXBLOCK kLeanMaxBlock
 #endif
-// ABL: profiling ablations (kernel modes 15..18, lean::scan_doc): stage A cut short, no stage B
-template <bool SHARED, int ABL = 0>
+// ABL: profiling ablations (kernel modes 15..18, lean::scan_doc): stage A cut short, no stage B.
+// FEAT: the walker features the ruleset needs (RulesetHdr::lean_feat: kLeanArr | kLeanCaps)
+template <bool SHARED, int ABL = 0, int FEAT = 3>
 __global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_lean(
     const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
     const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens, uint32_t n,
@@ -46,7 +47,8 @@ __global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_le
     if (ok) {
         const uint32_t mis = (uint32_t)((uintptr_t)d & 15u);
         lean::DmaLoader ld{reinterpret_cast<const uint4*>(d - mis), (len + mis + 15u) / 16u, wring};
-        ok = lean::scan_doc<ABL>(blob, len, mis, row, wring + (threadIdx.x & 63u) * 16u, ld, dec, keep_rows);
+        ok = lean::scan_doc<ABL, (FEAT & kLeanArr) != 0, (FEAT & kLeanCaps) != 0>(
+            blob, len, mis, row, wring + (threadIdx.x & 63u) * 16u, ld, dec, keep_rows);
     } else {
         row[0] = kRowSlow;
     }
@@ -76,22 +78,20 @@ static uint32_t lean_block(uint32_t blob_bytes) {
     return best ? best : 256u;
 }
 
+#define AJX_LEAN_K(SH, A, F) reinterpret_cast<const void*>(&ajx_scan_lean<SH, A, F>)
 hipError_t launch_lean(const uint8_t* const* d_sets, uint32_t shared_blob_bytes, const uint8_t* d_arena,
                        const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint64_t* d_rows,
                        uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, uint8_t* d_tri,
                        int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream, int abl,
-                       const uint32_t* d_perm, bool keep_rows) {
+                       const uint32_t* d_perm, bool keep_rows, uint32_t lean_feat) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0;
     static std::atomic<uint64_t> attr_done{0};
     hipError_t e = attr_once(attr_done, [] {
-        const void* ks[] = {reinterpret_cast<const void*>(&ajx_scan_lean<true>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<false>),
+        const void* ks[] = {AJX_LEAN_K(true, 0, 2), AJX_LEAN_K(true, 0, 3), AJX_LEAN_K(false, 0, 3),
 #if defined(AJX_LEAN_ABLATIONS)
-                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 1>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 2>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 3>),
-                            reinterpret_cast<const void*>(&ajx_scan_lean<true, 4>)
+                            AJX_LEAN_K(true, 1, 2), AJX_LEAN_K(true, 2, 2), AJX_LEAN_K(true, 3, 2), AJX_LEAN_K(true, 4, 2),
+                            AJX_LEAN_K(true, 1, 3), AJX_LEAN_K(true, 2, 3), AJX_LEAN_K(true, 3, 3), AJX_LEAN_K(true, 4, 3)
 #endif
         };
         for (const void* k : ks) {
@@ -106,29 +106,36 @@ hipError_t launch_lean(const uint8_t* const* d_sets, uint32_t shared_blob_bytes,
     const uint32_t lgrid = (n + lblock - 1) / lblock;
     const uint32_t llds = ring_off + (lblock / 64) * lean::kRingBytesPerWave;
     const uint32_t keep = keep_rows ? 1u : 0u;
+    // (two instances: without and with array walking. The capture-free instances cost
+    // the walk loop scratch reloads of spilled scalar registers, which wait behind the
+    // ring's loads in flight: measured slower, c2 1.39 against 1.27 ms)
+    const uint32_t feat = (lean_feat & kLeanArr) ? 3u : 2u;
+    using K = void (*)(const uint8_t* const*, const uint32_t*, const uint8_t*, const uint64_t*, const uint32_t*,
+                       uint32_t, uint64_t*, uint32_t, uint32_t*, uint32_t*, uint8_t*, int32_t*, uint64_t*, uint32_t,
+                       uint32_t, const uint32_t*, uint32_t);
+    K k = nullptr;
     if (abl) {
 #if defined(AJX_LEAN_ABLATIONS)
         if (!shared || abl > 4) return hipErrorInvalidValue;
-        auto k = abl == 1 ? &ajx_scan_lean<true, 1> : abl == 2 ? &ajx_scan_lean<true, 2>
-               : abl == 3 ? &ajx_scan_lean<true, 3> : &ajx_scan_lean<true, 4>;
-        hipLaunchKernelGGL(k, dim3(lgrid), dim3(lblock), llds, stream, d_sets, nullptr, d_arena, d_offs, d_lens, n,
-                           d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, ring_off, d_perm,
-                           keep);
-        return hipGetLastError();
+        const bool f2 = feat == 2;
+        k = abl == 1 ? (f2 ? &ajx_scan_lean<true, 1, 2> : &ajx_scan_lean<true, 1, 3>)
+          : abl == 2 ? (f2 ? &ajx_scan_lean<true, 2, 2> : &ajx_scan_lean<true, 2, 3>)
+          : abl == 3 ? (f2 ? &ajx_scan_lean<true, 3, 2> : &ajx_scan_lean<true, 3, 3>)
+                     : (f2 ? &ajx_scan_lean<true, 4, 2> : &ajx_scan_lean<true, 4, 3>);
 #else
         return hipErrorInvalidValue;  // (a profiling build: scripts/build_variant.sh NAME -DAJX_LEAN_ABLATIONS)
 #endif
+    } else if (!shared) {
+        k = &ajx_scan_lean<false, 0, 3>;
+    } else {
+        k = feat == 2 ? &ajx_scan_lean<true, 0, 2> : &ajx_scan_lean<true, 0, 3>;
     }
-    if (shared)
-        hipLaunchKernelGGL((ajx_scan_lean<true>), dim3(lgrid), dim3(lblock), llds, stream, d_sets, nullptr, d_arena,
-                           d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride,
-                           ring_off, d_perm, keep);
-    else
-        hipLaunchKernelGGL((ajx_scan_lean<false>), dim3(lgrid), dim3(lblock), llds, stream, d_sets, nullptr, d_arena,
-                           d_offs, d_lens, n, d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride,
-                           ring_off, d_perm, keep);
+    hipLaunchKernelGGL(k, dim3(lgrid), dim3(lblock), llds, stream, d_sets, nullptr, d_arena, d_offs, d_lens, n,
+                       d_rows, row_stride, d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, ring_off, d_perm,
+                       keep);
     return hipGetLastError();
 }
+#undef AJX_LEAN_K
 
 // The single-pass kernel for multi-tenant batches (one ruleset per request through
 // set_of_req; the caller buckets requests by AuthConfig, so a workgroup's requests form a

@@ -512,7 +512,6 @@ class BatchTimeout(AuthjxError):
 
 
 _batcher_knob_lock = threading.Lock()
-_BATCHER_DEFAULT_WORKERS = 2  # (ajx_api.cpp g_batcher_workers' default; only this module changes it)
 
 
 class Batcher:
@@ -531,15 +530,17 @@ class Batcher:
         # reads: set, create and restore under one lock, so that batchers created at the
         # same time in other threads keep the count they asked for)
         with _batcher_knob_lock:
+            prev = 0
             if workers:
                 L.authjx_debug_batcher_workers.argtypes = [C.c_uint32]
+                prev = L.authjx_debug_batcher_workers(0)  # (0: the current count, restored below)
                 _check(L.authjx_debug_batcher_workers(int(workers)), "authjx_debug_batcher_workers")
             try:
                 _check(L.authjx_batcher_create(ctx._h, max_batch, window_us, queue_cap, C.byref(h)),
                        "authjx_batcher_create")
             finally:
-                if workers:
-                    L.authjx_debug_batcher_workers(_BATCHER_DEFAULT_WORKERS)
+                if workers and prev > 0:
+                    L.authjx_debug_batcher_workers(prev)
         self.ctx = ctx
         self._h = h
         ctx._batchers.add(self)

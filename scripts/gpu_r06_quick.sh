@@ -17,4 +17,9 @@ for wl in ${WLS:-c2 c3}; do
   fi
   done
 done
-echo done
+
+for wl in $BENCH_WLS; do
+  timeout -k 10 300 python -u bench.py --workload $wl --steps 10 --warmup 3 --cpu-seconds 3 --no-pcie --no-serve > $O/bench_$wl.log 2>&1 || { echo "bench $wl failed"; tail -20 $O/bench_$wl.log; exit 1; }
+  tail -1 $O/bench_$wl.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('$wl', d['ms_per_step'], d['value'], d.get('roofline',{}).get('frac'), d.get('parity'))"
+done
+echo bench-done

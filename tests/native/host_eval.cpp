@@ -295,7 +295,11 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
     const uint32_t nblk = (len + (mis & 15) + 15) / 16;
     lean::CopyLoader ld{(const uint8_t*)a, nblk, nb, ring_mem.data() + ((mis * 5u) & 63u) * 16u};
     uint64_t dec[2] = {0, 0};
-    const bool ok = lean::scan_doc(blob, len, (uint32_t)(mis & 15), row.data(), ld.lane_ring, ld, dec, g_lean_keep);
+    // (the instance the kernel takes for this ruleset: RulesetHdr::lean_feat)
+    const uint32_t m15 = (uint32_t)(mis & 15), f = (hd->lean_feat & kLeanArr) ? 3u : 2u;
+    const RowRef rr(row.data());
+    const bool ok = f == 2 ? lean::scan_doc<0, false, true>(blob, len, m15, rr, ld.lane_ring, ld, dec, g_lean_keep)
+                           : lean::scan_doc<0, true, true>(blob, len, m15, rr, ld.lane_ring, ld, dec, g_lean_keep);
     g_last_dec[0] = dec[0];
     g_last_dec[1] = dec[1];
     if (!ok) return -1;

