@@ -705,6 +705,11 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
 
     // ---- assemble ----
     Builder b;
+    bool sd_on = false;  // the streaming scan's tables, appended after the hot prefix
+    StreamHdr sd_sh;
+    std::vector<StreamKeySlot> sd_k;
+    std::vector<StreamPathSlot> sd_p;
+    std::vector<StreamTail> sd_t;
     RulesetHdr hdr;
     std::memset(&hdr, 0, sizeof hdr);
     b.append(&hdr, sizeof hdr);
@@ -993,17 +998,13 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
                 sh.exact_hi = (uint32_t)(sexact >> 32);
                 sh.n_rec = nrec;
                 sh.n_tails = (uint32_t)tails.size();
-                hdr.off_stream = (uint32_t)b.align16();
-                b.append(&sh, sizeof sh);
-                StreamHdr* shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
-                shp->off_keys = (uint32_t)b.align16();
-                b.append(kslots.data(), kslots.size() * sizeof(StreamKeySlot));
-                shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
-                shp->off_paths = (uint32_t)b.align16();
-                b.append(pslots.data(), pslots.size() * sizeof(StreamPathSlot));
-                shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
-                shp->off_tails = (uint32_t)b.align16();
-                b.append(tails.data(), tails.size() * sizeof(StreamTail));
+                // (appended after hot_bytes: only the streaming kernel reads them, and it
+                // stages the whole blob; the multi-tenant kernel's staged prefix stays small)
+                sd_on = true;
+                sd_sh = sh;
+                sd_k = kslots;
+                sd_p = pslots;
+                sd_t = tails;
             }
         }
         std::vector<SelectorPatterns> sp(sels.size());
@@ -1067,6 +1068,19 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     b.append(pats.data(), pats.size() * sizeof(Pattern));
     // the exact scan's tables last: the multi-tenant kernel stages only [0, hot_bytes)
     hdr.hot_bytes = (uint32_t)b.align16();
+    if (sd_on) {
+        hdr.off_stream = (uint32_t)b.align16();
+        b.append(&sd_sh, sizeof sd_sh);
+        StreamHdr* shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
+        shp->off_keys = (uint32_t)b.align16();
+        b.append(sd_k.data(), sd_k.size() * sizeof(StreamKeySlot));
+        shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
+        shp->off_paths = (uint32_t)b.align16();
+        b.append(sd_p.data(), sd_p.size() * sizeof(StreamPathSlot));
+        shp = reinterpret_cast<StreamHdr*>(b.blob.data() + hdr.off_stream);
+        shp->off_tails = (uint32_t)b.align16();
+        b.append(sd_t.data(), sd_t.size() * sizeof(StreamTail));
+    }
     hdr.off_modifiers = (uint32_t)b.align16();
     b.append(mods.data(), mods.size() * sizeof(Modifier));
     hdr.off_selectors = (uint32_t)b.align16();

@@ -145,7 +145,7 @@ hipError_t launch_lean(const uint8_t* const* d_sets, uint32_t shared_blob_bytes,
 // reads — as many as fit the staging region; a wave whose requests all fall in staged
 // runs reads every table from LDS (each lane from its own run's copy), any other wave
 // reads them from global memory. Dynamic LDS: [staging region (ring_off bytes)] [rings].
-constexpr uint32_t kTenantRuns = 8;  // runs a workgroup may stage
+constexpr uint32_t kTenantRuns = 16;  // runs a workgroup may stage
 static_assert(lean::kRingBytesPerWave == kWinRingBytesPerWave, "the tenant kernel's rings serve both scans");
 __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_tenant(
     const uint8_t* const* __restrict__ sets, const uint32_t* __restrict__ set_of_req,
@@ -224,21 +224,16 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
             }
             return;
         }
-        const uint8_t* blob = reinterpret_cast<const uint8_t*>(s_stage) + my_off;
-        if (k >= n) return;
-        if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off)) ||
-            !finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
-            row[0] = kRowSlow;
-            slow_ids[atomicAdd(slow_count, 1u)] = r;
-        }
-    } else {
-        const uint8_t* gblob = sets[sid];
-        if (k >= n) return;
-        if (!scan_request<0>(gblob, d, lens[r], row, lane_ring(ring_off)) ||
-            !finish_request(r, gblob, d, row, out_tri, out_err, out_bm, stride)) {
-            row[0] = kRowSlow;
-            slow_ids[atomicAdd(slow_count, 1u)] = r;
-        }
+    }
+    // a wave of several rulesets, or of rulesets not staged: the token scanner, each lane on
+    // its own ruleset (its staged copy or the global blob: one generic pointer, one copy of
+    // the scanner and of stage B in the kernel, which keeps the lean path's registers)
+    const uint8_t* blob = ridx < nst ? reinterpret_cast<const uint8_t*>(s_stage) + my_off : sets[sid];
+    if (k >= n) return;
+    if (!scan_request<0>(blob, d, lens[r], row, lane_ring(ring_off)) ||
+        !finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride)) {
+        row[0] = kRowSlow;
+        slow_ids[atomicAdd(slow_count, 1u)] = r;
     }
 }
 
@@ -253,12 +248,12 @@ hipError_t launch_tenant(const uint8_t* const* d_sets, const uint32_t* d_set_of_
         // uses, the staging region + four window rings)
         return hipFuncSetAttribute(reinterpret_cast<const void*>(&ajx_scan_fused_tenant),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   kMaxTenantStageBytes + 4 * kWinRingBytesPerWave);
+                                   kMaxTenantStageBytes + (kTenantBlock / 64) * kWinRingBytesPerWave);
     });
     if (e != hipSuccess) return e;
-    // 4-wave workgroups, so more of them fall inside one AuthConfig's bucket (staging region:
-    // the tenant budget less room for the kernel's static LDS, so four groups still fit a CU)
-    const uint32_t tblock = 256, tgrid = (n + tblock - 1) / tblock;
+    // (staging region: the tenant budget less room for the kernel's static LDS, so two
+    // groups still fit a CU)
+    const uint32_t tblock = kTenantBlock, tgrid = (n + tblock - 1) / tblock;
     const uint32_t toff = kMaxTenantStageBytes - 256u;
     hipLaunchKernelGGL(ajx_scan_fused_tenant, dim3(tgrid), dim3(tblock), toff + (tblock / 64) * kWinRingBytesPerWave,
                        stream, d_sets, d_set_of_req, d_arena, d_offs, d_lens, n, d_rows, row_stride, d_slow_count,

@@ -261,6 +261,17 @@ static int eval_single_pass(void* h, const uint8_t* doc, uint32_t len, uint32_t 
 }
 
 extern "C" uint32_t ht_blob_size(void* h) { return (uint32_t)((HtRuleset*)h)->c.blob.size(); }
+// the ruleset's header (profiling helpers): key table log2 size, probes, hot bytes
+extern "C" void ht_blob_keytab(void* h, uint32_t* out) {
+    const RulesetHdr* hd = (const RulesetHdr*)((HtRuleset*)h)->c.blob.data();
+    out[0] = hd->key_slots_log2;
+    out[1] = hd->key_probes;
+    out[2] = hd->hot_bytes;
+    out[3] = hd->n_trie_nodes;
+    out[4] = hd->off_key_slots;
+    out[5] = hd->off_eager;
+}
+extern "C" uint32_t ht_blob_hot_bytes(void* h) { return ((const RulesetHdr*)((HtRuleset*)h)->c.blob.data())->hot_bytes; }
 
 
 
