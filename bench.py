@@ -87,6 +87,18 @@ def host_threads() -> int:
     return max(1, min(n, cap) if cap > 0 else n)
 
 
+def host_cores() -> dict:
+    """The host's core count beside the threads the baseline used: the north star asks for
+    the reference timed with GOMAXPROCS = host cores; the GPU box gives a process its
+    per-GPU share (OMP_NUM_THREADS), which the baseline stays within."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    return {"host_cores": os.cpu_count(), "affinity_cores": aff,
+            "threads_cap": int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None}
+
+
 def cpu_baseline(w, rpr, target_s, gpu_tri, gpu_bm):
     """Oracle (C restatement, oracle/) on a bounded sample of the same workload; also the
     parity check of the GPU results on that sample."""
@@ -119,6 +131,7 @@ def cpu_baseline(w, rpr, target_s, gpu_tri, gpu_bm):
         "unit": "request×rule evals/s",
         "decisions_per_s": reps * sample / dt,
         "cores": threads,
+        **host_cores(),
         "kind": "port",
         "sample": f"first {sample} of the {w.n} synthetic docs x {reps} passes, same ruleset, oracle/ C "
                   f"restatement (gjson re-scan per pattern like the reference, each pattern evaluated once), "
@@ -147,7 +160,7 @@ def phase_cpu_baseline(w, exprs, target_s, gpu_tri):
     got = np.stack(outs, axis=1)
     mism = int((got != gpu_tri[:k]).any(axis=1).sum())
     return {"value": k * R / dt, "unit": "request×rule evals/s", "decisions_per_s": k / dt, "cores": threads,
-            "kind": "port", "sample": f"first {k} of the {w.n} docs, every tree of the phase, oracle/ C restatement, "
+            **host_cores(), "kind": "port", "sample": f"first {k} of the {w.n} docs, every tree of the phase, oracle/ C restatement, "
                                       f"{threads} host threads, {dt:.1f}s"}, {"sample": k, "mismatches": mism}
 
 
@@ -387,7 +400,7 @@ def main():
     if phase:
         algo_bytes += w.n * len(sel.paths) * 12
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_note = None, None
+    traffic, traffic_note, traffic_src = None, None, None
     try:
         with open(args.pmc_json) as f:
             pmc = json.load(f).get(args.workload, {})
@@ -400,6 +413,8 @@ def main():
                 (kname != "ajx_scan_fused" or "tenant" not in pmc.get("kernel", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_note = pmc.get("note")
+            traffic_src = {"file": os.path.relpath(args.pmc_json, ROOT), "kernel": pmc.get("kernel_names") or
+                           pmc.get("kernel"), "commit": pmc.get("commit")}
     except (OSError, ValueError):
         pass
 
@@ -513,6 +528,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
                 "traffic_note": traffic_note,
+                "traffic_source": traffic_src,  # (the PMC file's kernel instance and commit)
                 "kernel_ms": kern_ms,
                 **({"note": "kernel_ms is the whole step's event time, decision all-gather included"}
                    if gather else {}),

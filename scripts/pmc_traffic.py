@@ -18,21 +18,40 @@ import statistics
 import sys
 
 
-def per_launch(d, counter, kernel_sub):
+def per_launch(d, counter, kernel_sub, names=None):
     vals = []
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if kernel_sub in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]) * 1024.0)
+                if names is not None:
+                    names.add(r["Kernel_Name"])
     return statistics.median(vals) if vals else None, len(vals)
+
+
+def source_commit():
+    """The commit the counters were taken on: $AJX_COMMIT (set by the GPU scripts from the
+    checkout the box ran), else git's HEAD here."""
+    import os
+    import subprocess
+
+    c = os.environ.get("AJX_COMMIT")
+    if c:
+        return c
+    try:
+        return subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True,
+                              check=True).stdout.strip()
+    except (OSError, subprocess.CalledProcessError):
+        return None
 
 
 def main():
     fetch_dir, write_dir, workload, n = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
     out = sys.argv[5] if len(sys.argv) > 5 else "pmc_traffic.json"
     kernel = sys.argv[6] if len(sys.argv) > 6 else "ajx_scan_fused"
-    fb, nf = per_launch(fetch_dir, "FETCH_SIZE", kernel)
-    wb, nw = per_launch(write_dir, "WRITE_SIZE", kernel)
+    names = set()
+    fb, nf = per_launch(fetch_dir, "FETCH_SIZE", kernel, names)
+    wb, nw = per_launch(write_dir, "WRITE_SIZE", kernel, names)
     try:
         with open(out) as f:
             allw = json.load(f)
@@ -46,6 +65,8 @@ def main():
         "workload": workload,
         "n": n,
         "kernel": kernel,
+        "kernel_names": sorted(names),
+        "commit": source_commit(),
         "fetch_bytes_per_launch_raw": fb,
         "fetch_calibration": k,
         "write_bytes_per_launch": wb,
