@@ -53,7 +53,17 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
                             int mode = 0, const uint32_t* d_perm = nullptr, bool mods = false,
-                            bool keep_rows = true, uint32_t lean_feat = 3);
+                            bool keep_rows = true, uint32_t lean_feat = 3, const uint32_t* d_pos_of = nullptr,
+                            uint8_t* d_tout = nullptr, uint32_t n_out = 1);
+// (d_pos_of, d_tout: with d_perm, the lean kernel writes its outputs to d_tout in work-item
+// order, tri-states | error indices | bitmaps at 256-byte aligned offsets
+// (tout_bytes), and ajx_unpermute gathers them to request order by d_pos_of
+// (launch_len_order); n_out: results per request)
+inline size_t tout_bytes(uint32_t n, uint32_t n_out, uint32_t stride) {
+    const size_t a = ((size_t)n * n_out + 255u) & ~(size_t)255u;
+    const size_t b = ((size_t)n * n_out * 4u + 255u) & ~(size_t)255u;
+    return a + b + (size_t)n * stride * 8u;
+}
 
 // The lean single-pass kernel (ajx_lean.hip, one ruleset for the batch): stage A with the
 // lean scan and stage B per work-item; requests it can not prove go to d_slow_ids (the
@@ -65,7 +75,7 @@ hipError_t launch_lean(const uint8_t* const* d_sets, uint32_t shared_blob_bytes,
                        const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint64_t* d_rows,
                        uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, uint8_t* d_tri,
                        int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream, int abl,
-                       const uint32_t* d_perm, bool keep_rows, uint32_t lean_feat);
+                       const uint32_t* d_perm, bool keep_rows, uint32_t lean_feat, bool out_k = false);
 
 // The multi-tenant single-pass kernel (ajx_lean.hip): each workgroup stages its runs'
 // rulesets in LDS; waves of one staged ruleset run the lean scan, others the token scanner.
@@ -98,7 +108,8 @@ hipError_t launch_eval_stream(const uint8_t* const* d_sets, const uint32_t* d_se
 
 // Length-bucketed request order for the single-pass kernel: d_perm[n] = request ids,
 // longest 8-byte length class first; d_hist needs 2 * 1024 + 1 u32 of scratch.
+// d_pos_of (optional): n u32, the inverse (work-item of each request).
 hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist, uint32_t* d_perm,
-                            hipStream_t stream);
+                            hipStream_t stream, uint32_t* d_pos_of = nullptr);
 
 }  // namespace ajx

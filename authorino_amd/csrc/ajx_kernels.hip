@@ -709,15 +709,21 @@ __global__ __launch_bounds__(kLenBuckets) void ajx_len_scan(const uint32_t* __re
     if (t == 0) cursor[kLenBuckets] = (hi < lo || hi - lo < kLenSpreadMin) ? 1u : 0u;
 }
 
-// perm[cursor[class] + rank] = request; one global atomic per (workgroup, class)
+// perm[cursor[class] + rank] = request; one global atomic per (workgroup, class).
+// pos_of (optional): pos_of[request] = its work-item, written in request order (coalesced),
+// for the gather that puts work-item-ordered outputs back in request order (ajx_unpermute)
 __global__ __launch_bounds__(kLenBuckets) void ajx_len_scatter(const uint32_t* __restrict__ lens, uint32_t n,
                                                                uint32_t* __restrict__ cursor,
-                                                               uint32_t* __restrict__ perm) {
+                                                               uint32_t* __restrict__ perm,
+                                                               uint32_t* __restrict__ pos_of) {
     __shared__ uint32_t cnt[kLenBuckets];
     __shared__ uint32_t base[kLenBuckets];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (cursor[kLenBuckets]) {  // narrow length spread: keep the caller's order
-        if (i < n) perm[i] = i;
+        if (i < n) {
+            perm[i] = i;
+            if (pos_of) pos_of[i] = i;
+        }
         return;
     }
     cnt[threadIdx.x] = 0;
@@ -730,11 +736,34 @@ __global__ __launch_bounds__(kLenBuckets) void ajx_len_scatter(const uint32_t* _
     __syncthreads();
     if (cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
     __syncthreads();
-    if (i < n) perm[base[b] + rank] = i;
+    if (i < n) {
+        perm[base[b] + rank] = i;
+        if (pos_of) pos_of[i] = base[b] + rank;
+    }
+}
+
+// outputs written in work-item order (t_*) back to request order: request i's results are
+// work-item pos_of[i]'s. One thread per request, so the stores are coalesced; the loads are
+// a gather over the work-item-ordered copies (n x (n_out x 5 + stride x 8) bytes, mostly
+// still in L2 / MALL behind the kernel that wrote them).
+__global__ __launch_bounds__(256) void ajx_unpermute(const uint32_t* __restrict__ pos_of, uint32_t n, uint32_t n_out,
+                                                     uint32_t stride, const uint8_t* __restrict__ t_tri,
+                                                     const int32_t* __restrict__ t_err,
+                                                     const uint64_t* __restrict__ t_bm, uint8_t* __restrict__ tri,
+                                                     int32_t* __restrict__ err, uint64_t* __restrict__ bm) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const size_t j = pos_of[i];
+    for (uint32_t q = 0; q < n_out; q++) {
+        tri[(size_t)i * n_out + q] = t_tri[j * n_out + q];
+        if (err) err[(size_t)i * n_out + q] = t_err[j * n_out + q];
+    }
+    if (bm)
+        for (uint32_t w = 0; w < stride; w++) bm[(size_t)i * stride + w] = t_bm[j * stride + w];
 }
 
 hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist, uint32_t* d_perm,
-                            hipStream_t stream) {
+                            hipStream_t stream, uint32_t* d_pos_of) {
     hipError_t e = hipMemsetAsync(d_hist, 0, (2 * kLenBuckets + 1) * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     const uint32_t blocks = (n + kLenBuckets - 1) / kLenBuckets;
@@ -742,7 +771,7 @@ hipError_t launch_len_order(const uint32_t* d_lens, uint32_t n, uint32_t* d_hist
                        d_hist);
     hipLaunchKernelGGL(ajx_len_scan, dim3(1), dim3(kLenBuckets), 0, stream, d_hist, d_hist + kLenBuckets);
     hipLaunchKernelGGL(ajx_len_scatter, dim3(blocks), dim3(kLenBuckets), 0, stream, d_lens, n, d_hist + kLenBuckets,
-                       d_perm);
+                       d_perm, d_pos_of);
     return hipGetLastError();
 }
 
@@ -911,7 +940,8 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
                             const uint8_t* d_arena, const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n,
                             uint8_t* d_tri, int32_t* d_err, uint64_t* d_bm, uint32_t stride, uint64_t* d_rows,
                             uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, hipStream_t stream,
-                            int mode, const uint32_t* d_perm, bool mods, bool keep_rows, uint32_t lean_feat) {
+                            int mode, const uint32_t* d_perm, bool mods, bool keep_rows, uint32_t lean_feat,
+                            const uint32_t* d_pos_of, uint8_t* d_tout, uint32_t n_out) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0 && d_set_of_req == nullptr;
     // workgroup size by the waves a CU holds (each workgroup stages its own blob copy)
@@ -972,10 +1002,23 @@ hipError_t launch_eval_fast(const uint8_t* const* d_sets, const uint32_t* d_set_
         // scan with per-lane table parameters took 6.39 ms and one pass per ruleset of a
         // wave 7.3-7.8 ms, against 5.38 ms for the tenant kernel's LDS-staged tables)
         if (mode >= 15 && !shared) return hipErrorInvalidValue;
+        // in length order, the outputs go to d_tout in work-item order and are gathered back
+        // (ajx_unpermute) before the exact scan writes its requests' own
+        const bool out_k = d_perm && d_pos_of && d_tout && mode < 15;
+        const size_t o_err = ((size_t)n * n_out + 255u) & ~(size_t)255u;
+        const size_t o_bm = o_err + (((size_t)n * n_out * 4u + 255u) & ~(size_t)255u);
+        uint8_t* k_tri = out_k ? d_tout : d_tri;
+        int32_t* k_err = out_k ? (d_err ? reinterpret_cast<int32_t*>(d_tout + o_err) : nullptr) : d_err;
+        uint64_t* k_bm = out_k ? (d_bm ? reinterpret_cast<uint64_t*>(d_tout + o_bm) : nullptr) : d_bm;
         e = launch_lean(d_sets, shared ? shared_blob_bytes : 0u, d_arena, d_offs, d_lens, n, d_rows, row_stride,
-                        d_slow_count, d_slow_ids, d_tri, d_err, d_bm, stride, stream, mode >= 15 ? mode - 14 : 0,
-                        d_perm, keep_rows, lean_feat);
+                        d_slow_count, d_slow_ids, k_tri, k_err, k_bm, stride, stream, mode >= 15 ? mode - 14 : 0,
+                        d_perm, keep_rows, lean_feat, out_k);
         if (e != hipSuccess || mode >= 15) return e;
+        if (out_k) {
+            hipLaunchKernelGGL(ajx_unpermute, dim3((n + 255u) / 256u), dim3(256), 0, stream, d_pos_of, n, n_out,
+                               stride, k_tri, k_err, k_bm, d_tri, d_err, d_bm);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
     } else if (shared_blob_bytes) {
         // multi-tenant batch (shared_blob_bytes != 0: staging on): each workgroup stages its
         // runs' rulesets, those that fit (ajx_scan_fused_tenant);

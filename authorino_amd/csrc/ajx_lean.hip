@@ -34,6 +34,9 @@ __global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_le
     uint32_t keep_rows) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t r = k < n ? (perm ? perm[k] : k) : 0u;
+    // keep_rows bit 1: the outputs in work-item order (gathered back by ajx_unpermute)
+    const uint32_t o = (keep_rows & 2u) ? k : r;
+    keep_rows &= 1u;
     const uint8_t* blob = stage_blob<SHARED>(sets[SHARED || !set_of_req ? 0 : set_of_req[r]]);
     if (k >= n) return;
     extern __shared__ uint4 s_lean_dyn[];
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_le
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
-    if (!finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec)) {
+    if (!finish_request(o, blob, d, row, out_tri, out_err, out_bm, stride, dec)) {
         row[0] = kRowSlow;
         slow_ids[atomicAdd(slow_count, 1u)] = r;
     }
@@ -83,7 +86,7 @@ hipError_t launch_lean(const uint8_t* const* d_sets, uint32_t shared_blob_bytes,
                        const uint64_t* d_offs, const uint32_t* d_lens, uint32_t n, uint64_t* d_rows,
                        uint32_t row_stride, uint32_t* d_slow_count, uint32_t* d_slow_ids, uint8_t* d_tri,
                        int32_t* d_err, uint64_t* d_bm, uint32_t stride, hipStream_t stream, int abl,
-                       const uint32_t* d_perm, bool keep_rows, uint32_t lean_feat) {
+                       const uint32_t* d_perm, bool keep_rows, uint32_t lean_feat, bool out_k) {
     if (n == 0) return hipSuccess;
     const bool shared = shared_blob_bytes != 0;
     static std::atomic<uint64_t> attr_done{0};
@@ -105,7 +108,7 @@ hipError_t launch_lean(const uint8_t* const* d_sets, uint32_t shared_blob_bytes,
     const uint32_t lblock = shared ? lean_block(shared_blob_bytes) : 256u;
     const uint32_t lgrid = (n + lblock - 1) / lblock;
     const uint32_t llds = ring_off + (lblock / 64) * lean::kRingBytesPerWave;
-    const uint32_t keep = keep_rows ? 1u : 0u;
+    const uint32_t keep = (keep_rows ? 1u : 0u) | (out_k && d_perm ? 2u : 0u);
     // (two instances: without and with array walking. The capture-free instances cost
     // the walk loop scratch reloads of spilled scalar registers, which wait behind the
     // ring's loads in flight: measured slower, c2 1.39 against 1.27 ms)

@@ -521,26 +521,33 @@ class Batcher:
     GIL around the blocking call, so Python threads wait concurrently."""
 
     def __init__(self, ctx: "Context", max_batch: int = 4096, window_us: int = 200, queue_cap: int = 0,
-                 workers: int = 0):
+                 workers: int = 0, modes=None):
         """workers: worker threads, each with its own stream (0: the library's default, 2;
-        profiling knob, authjx_debug_batcher_workers, not part of authjx.h)."""
+        profiling knob, authjx_debug_batcher_workers, not part of authjx.h). modes: None, or
+        (wake, sync, zero-copy) for authjx_debug_batcher_modes (profiling; the library's
+        default modes, (0, 0, 1), are restored afterwards)."""
         L = load_library()
         h = C.c_void_p()
-        # (the worker count is a process-wide knob of the library that batcher creation
-        # reads: set, create and restore under one lock, so that batchers created at the
-        # same time in other threads keep the count they asked for)
+        # (the worker count and modes are process-wide knobs of the library that batcher
+        # creation reads: set, create and restore under one lock, so that batchers created
+        # at the same time in other threads keep what they asked for)
         with _batcher_knob_lock:
             prev = 0
             if workers:
                 L.authjx_debug_batcher_workers.argtypes = [C.c_uint32]
                 prev = L.authjx_debug_batcher_workers(0)  # (0: the current count, restored below)
                 _check(L.authjx_debug_batcher_workers(int(workers)), "authjx_debug_batcher_workers")
+            if modes is not None:
+                L.authjx_debug_batcher_modes.argtypes = [C.c_uint32] * 3
+                _check(L.authjx_debug_batcher_modes(*[int(m) for m in modes]), "authjx_debug_batcher_modes")
             try:
                 _check(L.authjx_batcher_create(ctx._h, max_batch, window_us, queue_cap, C.byref(h)),
                        "authjx_batcher_create")
             finally:
                 if workers and prev > 0:
                     L.authjx_debug_batcher_workers(prev)
+                if modes is not None:
+                    L.authjx_debug_batcher_modes(0, 0, 1)
         self.ctx = ctx
         self._h = h
         ctx._batchers.add(self)
@@ -582,6 +589,21 @@ class Batcher:
         v = [C.c_uint64() for _ in range(4)]
         _check(load_library().authjx_batcher_stats(self._h, *[C.byref(x) for x in v]), "authjx_batcher_stats")
         return dict(zip(("batches", "requests", "expired", "max_batch_seen"), (x.value for x in v)))
+
+    def profile(self) -> Dict[str, float]:
+        """Profiling: mean µs per request (queue wait, caller resume) and per batch
+        (evaluation, waking callers, packing, launch calls, device wait)."""
+        L = load_library()
+        L.authjx_debug_batcher_profile.argtypes = [C.c_void_p, C.c_void_p]
+        v = np.zeros(9, dtype=np.uint64)
+        _check(L.authjx_debug_batcher_profile(self._h, v.ctypes.data), "authjx_debug_batcher_profile")
+        nb, nr = max(int(v[0]), 1), max(int(v[1]), 1)
+        per_r = {"wait_us": v[2], "resume_us": v[5]}
+        per_b = {"eval_us": v[3], "wake_us": v[4], "pack_us": v[6], "launch_us": v[7], "sync_us": v[8]}
+        out = {"batches": int(v[0]), "requests": int(v[1])}
+        out.update({k: round(int(x) / nr / 1e3, 2) for k, x in per_r.items()})
+        out.update({k: round(int(x) / nb / 1e3, 2) for k, x in per_b.items()})
+        return out
 
     def close(self):
         if getattr(self, "_h", None):

@@ -19,7 +19,11 @@ struct Host {
 };
 }  // namespace
 
+uint32_t g_wake = 0;  // the BatchCore wake mode of batchers created afterwards
+
 extern "C" {
+
+void hb_set_wake(uint32_t mode) { g_wake = mode; }
 
 void* hb_create(uint32_t max_batch, uint32_t window_us, uint32_t queue_cap, uint32_t delay_us) {
     Host* h = new Host();
@@ -34,7 +38,7 @@ void* hb_create(uint32_t max_batch, uint32_t window_us, uint32_t queue_cap, uint
             for (uint32_t k = 0; k < r->n_out; k++)
                 r->out_tri[k] = (uint8_t)(r->doc[0] ^ (uint8_t)(uintptr_t)r->rs ^ (uint8_t)k);
         return 0;
-    });
+    }, 1, g_wake);
     return h;
 }
 

@@ -59,6 +59,7 @@ hipError_t hipStreamDestroy(hipStream_t s) {
     return hipSuccess;
 }
 hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamQuery(hipStream_t) { return hipSuccess; }
 hipError_t hipEventCreate(hipEvent_t* e) {
     *e = new ihipEvent_t();
     return hipSuccess;
@@ -119,7 +120,7 @@ hipError_t launch_select_rows(const uint8_t* const*, const uint8_t*, const uint6
 hipError_t launch_eval_fast(const uint8_t* const*, const uint32_t*, uint32_t, const uint8_t*, const uint64_t*,
                             const uint32_t*, uint32_t n, uint8_t* tri, int32_t* err, uint64_t* bm, uint32_t stride,
                             uint64_t* rows, uint32_t row_stride, uint32_t* slow_count, uint32_t*, hipStream_t, int,
-                            const uint32_t*, bool, bool) {
+                            const uint32_t*, bool, bool, uint32_t, const uint32_t*, uint8_t*, uint32_t) {
     *slow_count = n / 7;
     for (uint32_t r = 0; r < n; r++) rows[(size_t)r * row_stride] = r;
     results(n, tri, err, bm, stride);
@@ -143,9 +144,12 @@ hipError_t launch_eval_stream(const uint8_t* const*, const uint32_t*, uint32_t, 
     results(n, tri, err, bm, stride);
     return hipSuccess;
 }
-hipError_t launch_len_order(const uint32_t*, uint32_t n, uint32_t* hist, uint32_t* perm, hipStream_t) {
+hipError_t launch_len_order(const uint32_t*, uint32_t n, uint32_t* hist, uint32_t* perm, hipStream_t,
+                            uint32_t* pos_of) {
     hist[0] = n;
     for (uint32_t r = 0; r < n; r++) perm[r] = r;
+    if (pos_of)
+        for (uint32_t r = 0; r < n; r++) pos_of[r] = r;
     return hipSuccess;
 }
 

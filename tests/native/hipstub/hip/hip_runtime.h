@@ -6,7 +6,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
-enum hipError_t { hipSuccess = 0, hipErrorInvalidValue = 1, hipErrorOutOfMemory = 2, hipErrorNoDevice = 100 };
+enum hipError_t { hipSuccess = 0, hipErrorInvalidValue = 1, hipErrorOutOfMemory = 2, hipErrorNoDevice = 100, hipErrorNotReady = 600 };
 enum hipMemcpyKind { hipMemcpyHostToHost = 0, hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2,
                      hipMemcpyDeviceToDevice = 3, hipMemcpyDefault = 4 };
 struct ihipStream_t;
@@ -31,6 +31,7 @@ hipError_t hipMemsetAsync(void*, int, size_t, hipStream_t);
 hipError_t hipStreamCreateWithFlags(hipStream_t*, unsigned);
 hipError_t hipStreamDestroy(hipStream_t);
 hipError_t hipStreamSynchronize(hipStream_t);
+hipError_t hipStreamQuery(hipStream_t);
 hipError_t hipEventCreate(hipEvent_t*);
 hipError_t hipEventCreateWithFlags(hipEvent_t*, unsigned);
 hipError_t hipEventDestroy(hipEvent_t);

@@ -2,7 +2,8 @@
 stand-in evaluator (tests/native/batcher_host.cpp): concurrent producers each get their
 own result, batches form by size and by window, batches are ordered by ruleset and never
 mix result shapes, deadlines expire unevaluated requests (also while waiting for queue
-room). The device-backed batcher is tested in test_gpu_parity.py."""
+room). Every test runs under each wake mode (one condition variable per caller; one
+broadcast per batch; one futex word per caller; callers waking each other in a tree). The device-backed batcher is tested in test_gpu_parity.py."""
 import ctypes as C
 import os
 import subprocess
@@ -16,10 +17,12 @@ _NATIVE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
 ETIMEDOUT = -5
 
 
-@pytest.fixture(scope="module")
-def lib():
+@pytest.fixture(scope="module", params=[0, 1, 2, 3], ids=["wake-cv", "wake-broadcast", "wake-futex", "wake-tree"])
+def lib(request):
     subprocess.run(["make", "-s", "-C", _NATIVE, "libajx_batchtest.so"], check=True)
     L = C.CDLL(os.path.join(_NATIVE, "libajx_batchtest.so"))
+    L.hb_set_wake.argtypes = [C.c_uint32]
+    L.hb_set_wake(request.param)
     L.hb_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
     L.hb_create.restype = C.c_void_p
     L.hb_eval.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint8, C.c_uint64, C.POINTER(C.c_uint8)]

@@ -74,6 +74,44 @@ def test_workload_parity(ctx, workload, n):
     assert (tri == 3).sum() == 0
 
 
+@pytest.mark.parametrize("spread", ["narrow", "wide"])
+def test_outputs_gathered_to_request_order(ctx, spread):
+    """In length order the lean kernel writes its outputs in work-item order and
+    ajx_unpermute gathers them back by each request's work-item (pos_of from the length
+    sort), before the exact scan writes the requests it was handed: lengths in a 200-byte
+    band (the sort keeps the identity order) and over the whole c2 range, one request in 16
+    re-spaced so that it takes the exact scan, a 3-word bitmap stride; then the same batch
+    without the error and bitmap outputs."""
+    import torch
+
+    from authorino_amd import workloads as W
+
+    w = W.make("c2", n=12000)
+    idx = np.arange(w.n)
+    if spread == "narrow":
+        idx = np.nonzero((w.lens >= 900) & (w.lens < 1100))[0][:6000]
+    assert idx.size >= 4096
+    docs = [bytes(w.arena[w.offs[i]:w.offs[i] + w.lens[i]]) for i in idx]
+    docs = [d.replace(b'":', b'": ', 3) if j % 16 == 5 else d for j, d in enumerate(docs)]
+    lens = np.array([len(d) for d in docs], dtype=np.uint32)
+    offs = np.zeros(len(docs), dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    arena = np.frombuffer(b"".join(docs) + b"\0" * 64, dtype=np.uint8)
+    rs = ctx.compile_expression(w.expr)
+    tri, err, bm = ctx.eval_host_arena([rs], arena, offs, lens, bitmap_words=3)
+    otri, oerr, obm = _oracle(w.expr, arena, offs, lens)
+    assert ctx.last_exact_count() >= len(docs) // 16
+    assert np.array_equal(tri, otri)
+    assert np.array_equal(err, oerr)
+    assert np.array_equal(bm[:, :1], obm) and not bm[:, 1:].any()
+    dev = torch.device("cuda", 0)
+    t_tri = torch.full((len(docs),), 7, dtype=torch.uint8, device=dev)
+    ctx.eval_device([rs], torch.from_numpy(arena).to(dev), torch.from_numpy(offs.view(np.int64)).to(dev),
+                    torch.from_numpy(lens.view(np.int32)).to(dev), t_tri)
+    torch.cuda.synchronize()
+    assert np.array_equal(t_tri.cpu().numpy(), otri)
+
+
 def test_full_size_c2_properties(ctx):
     """BASELINE config c2 at full size (1M requests): bit-exact on a strided sample plus
     size-independent properties (decision == AND of the 16 pattern bits for an All of
