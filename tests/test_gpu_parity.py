@@ -246,6 +246,47 @@ def test_random_documents_and_selectors(ctx):
     assert checked > 5000
 
 
+def test_regex_spans_every_alignment(ctx):
+    """`matches` over spans read by 16-byte blocks (dfa_match_span): strings of 0..70 bytes
+    at every alignment of the document, ASCII and with 2-byte UTF-8 sequences at random
+    places (block boundaries among them), through the lean kernel (a 5000-request batch)
+    and the streaming kernel (300 requests); equal to the oracle."""
+    import json
+
+    rng = np.random.default_rng(41)
+    pats = [("v", 5, r"^[a-z]{3,40}$"), ("v", 5, "\u00e9"), ("v", 5, "x$"), ("v", 5, r"^(ab)+c?$"),
+            ("v", 5, r"(?i)A.*X"), ("w", 1, "z")]
+    nodes = [(0, -1, -1, i) for i in range(len(pats))]
+    root = -1
+    for i in reversed(range(len(pats))):
+        nodes.append((2, i, root, -1))
+        root = len(nodes) - 1
+    docs = []
+    for j in range(5000):
+        n = int(rng.integers(0, 71))
+        if j % 7 == 0:
+            t = "ab" * (n // 2) + ("c" if n % 2 else "")
+        else:
+            t = "".join(rng.choice(list("abcxAX"), size=n))
+        if j % 3 == 0 and n:
+            k = int(rng.integers(0, n))
+            t = t[:k] + rng.choice(["\u00e9", "\u00df"]) + t[k + 1:]
+        pad = "p" * int(rng.integers(0, 16))
+        docs.append(json.dumps({"pad": pad, "v": t, "w": "z"}, ensure_ascii=False, separators=(",", ":")).encode())
+    rs = ctx.compile(pats, nodes, root)
+    ors = O.Ruleset(pats, nodes, root)
+    for sub in (docs, docs[:300]):
+        lens = np.array([len(d) for d in sub], dtype=np.uint32)
+        offs = np.zeros(len(sub), dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1])
+        arena = np.frombuffer(b"".join(sub) + b"\0" * 64, dtype=np.uint8)
+        tri, err, bm = ctx.eval_host_arena([rs], arena, offs, lens)
+        otri, oerr, obm = O.eval_batch([ors], arena, offs, lens)
+        assert np.array_equal(tri, otri)
+        assert np.array_equal(err, oerr)
+        assert np.array_equal(bm, obm)
+
+
 def test_pipeline_batch_on_device():
     """The batched `when` + authorization phase (authorino_amd.pipeline) on the device
     against the same phase evaluated with the oracle (tests/test_pipeline_host.py)."""
