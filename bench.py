@@ -490,7 +490,7 @@ def main():
                 "batches": st["batches"] - b0, "max_batch_seen": st["max_batch_seen"], "max_batch": 8192,
                 "window_us": window_us, "workers": 2,
                 "equal_to_batch_results": bool(np.array_equal(stri, tri_h[:ns].astype(np.uint8))),
-                "note": "authjx_batcher_eval per request, blocking, from pageable host memory (H2D / D2H per batch)"})
+                "note": "authjx_batcher_eval per request, blocking, from pageable host memory (the batch packed into pinned staging that the kernel reads over PCIe and writes its results to: no copies)"})
 
     if rank == 0:
         line = {
