@@ -23,6 +23,7 @@ def lib(request):
     L = C.CDLL(os.path.join(_NATIVE, "libajx_batchtest.so"))
     L.hb_set_wake.argtypes = [C.c_uint32]
     L.hb_set_wake(request.param)
+    L.wake_mode = request.param
     L.hb_create.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
     L.hb_create.restype = C.c_void_p
     L.hb_eval.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint8, C.c_uint64, C.POINTER(C.c_uint8)]
@@ -130,7 +131,11 @@ def test_queue_room_wait_honours_the_deadline(lib):
 def test_two_workers_keep_each_requests_window(lib):
     """with two workers, a worker that wakes after the other one drained the queue
     waits for the NEW oldest request's window (it used to flush at the old deadline, sending
-    small batches early). 16 closed-loop producers and a 3 ms window: batches stay full."""
+    small batches early). 16 closed-loop producers and a 3 ms window: batches stay full.
+    (Not under the broadcast wake, a profiling mode: every batch wakes every waiting caller,
+    so batch sizes depend on the host's load.)"""
+    if lib.wake_mode == 1:
+        pytest.skip("broadcast wake: batch sizes depend on host load")
     h = lib.hb_create(64, 3000, 0, 300)
     done = []
 
