@@ -962,11 +962,12 @@ struct authjx_batcher {
     // profiling sums (ns): packing the staging buffer, launch calls, the wait for the device
     std::atomic<uint64_t> pack_ns{0}, launch_ns{0}, sync_ns{0};
 
-    // one batch (ordered by ruleset): pack, one copy in, one launch (worker `wid` only).
-    // The staging copy carries the documents, offsets, lengths, each request's ruleset
-    // index and the rulesets' blob pointers; the kernel writes the results into the pinned
-    // buffer itself (mapped host memory: no copy back), so a small batch is one copy, one
-    // kernel (its counters left zero by the last one on this stream) and a synchronize.
+    // one batch (ordered by ruleset): pack, one launch (worker `wid` only). The pinned
+    // staging buffer carries the documents, offsets, lengths, each request's ruleset index
+    // and the rulesets' blob pointers; the kernel reads them from it (mapped host memory;
+    // with zero-copy off, one copy into device memory first) and writes the results into
+    // it, so a small batch is one kernel (its counters left zero by the last one on this
+    // stream) and a synchronize.
     int evaluate(std::vector<ajx::BatchReq*>& reqs, uint32_t wid) {
         Lane& L = lanes[wid];
         hipStream_t stream = L.stream;
