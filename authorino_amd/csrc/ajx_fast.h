@@ -1070,12 +1070,107 @@ AJX_HD bool incl_hits(const uint8_t* doc, const ValueRef& v, const Pattern* pats
     return true;
 }
 
+// incl_hits on a copy of the array in the lane's 128-byte ring (the lean kernel's, free
+// once stage A is done; chunk-major: ring byte x at (x >> 4) * 1024 + (x & 15)). The array's
+// aligned 16-byte blocks (at most eight) are loaded together and stored to the ring, so the
+// element walk reads LDS: one memory latency per array instead of one per dependent read
+// (about five per element in incl_hits). Compact arrays of unescaped strings of at most 16
+// bytes only; 1: *hits as incl_hits gives it, 0: not handled here (the caller takes
+// incl_hits, which decides every other array the same way it always did).
+AJX_HD uint32_t incl_hits_ring(const uint8_t* doc, const ValueRef& v, const Pattern* pats, const uint16_t* plist,
+                               uint32_t begin, uint32_t cnt, const uint8_t* lits, uint8_t* ring, uint32_t* hits) {
+    if (v.type != T_JSON || v.end - v.start < 2) return 0;
+    const uint32_t mis = (uint32_t)((uintptr_t)(doc + v.start) & 15u);
+    const uint32_t nb = (mis + (v.end - v.start) + 15u) / 16u;
+    if (nb > 8) return 0;
+    {
+#if defined(__HIPCC__)
+        using V16 = uint4;
+#else
+        using V16 = Block16;
+#endif
+        const V16* a4 = reinterpret_cast<const V16*>(doc + v.start - mis);
+        V16 blk[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) blk[j] = a4[j < nb ? j : nb - 1u];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) *reinterpret_cast<V16*>(ring + j * 1024u) = blk[j];
+    }
+    auto rw = [&](uint32_t q) -> uint32_t {  // the aligned dword at ring offset q (garbage past 127)
+        q &= 127u;
+        return *reinterpret_cast<const uint32_t*>(ring + (((q & 0x70u) << 6) | (q & 15u)));
+    };
+    auto r32 = [&](uint32_t a) -> uint32_t {  // 4 bytes from ring offset a
+        const uint32_t q = a & ~3u, sh = a & 3u;
+        const uint32_t w0 = rw(q), w1 = rw(q + 4u);
+#if defined(__HIP_DEVICE_COMPILE__)
+        return __builtin_amdgcn_alignbyte(w1, w0, sh);
+#else
+        return sh ? (w0 >> (8 * sh)) | (w1 << (32 - 8 * sh)) : w0;
+#endif
+    };
+    auto rbyte = [&](uint32_t a) -> uint32_t { return rw(a & ~3u) >> (8 * (a & 3u)) & 0xFFu; };
+    const uint32_t end = mis + (v.end - v.start) - 1u;  // the ']' (ring offset)
+    if (rbyte(mis) != '[' || rbyte(end) != ']') return 0;
+    uint32_t h = 0, i = mis + 1u;
+    while (i < end) {
+        if (rbyte(i) != '"') return 0;  // (other elements: incl_hits)
+        uint32_t k = i + 1u;
+        for (;;) {  // the closing quote: the first '"' or '\\' after i
+            if (k >= end) return 0;
+            const uint32_t w = r32(k);
+            const uint32_t m = end - k >= 4 ? 0xFFFFFFFFu : (1u << (8 * (end - k))) - 1u;
+            const uint32_t f = (eq_bytes(w, 0x22222222u) | eq_bytes(w, 0x5C5C5C5Cu)) & m;
+            if (f) {
+                k += (uint32_t)__builtin_ctz(f) >> 3;
+                break;
+            }
+            k += 4;
+        }
+        if (rbyte(k) != '"') return 0;  // an escape
+        const uint32_t n = k - i - 1u;
+        if (n > 16) return 0;
+        // the element's bytes [i + 1, k) as four masked dwords
+        uint32_t e[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t left = n > 4 * q ? n - 4 * q : 0u;
+            const uint32_t m = left >= 4 ? 0xFFFFFFFFu : (1u << (8 * left)) - 1u;
+            e[q] = left ? r32(i + 1u + 4 * q) & m : 0u;
+        }
+        for (uint32_t j = 0; j < cnt; j++) {
+            const Pattern pt = pats[plist[begin + j]];
+            if ((pt.op != OP_INCL && pt.op != OP_EXCL) || pt.state != P_OK || pt.lit_len != n) continue;
+            const uint32_t* lw = reinterpret_cast<const uint32_t*>(lits + pt.lit_off);  // (4-byte aligned)
+            bool eq = true;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint32_t left = n > 4 * q ? n - 4 * q : 0u;
+                const uint32_t m = left >= 4 ? 0xFFFFFFFFu : (1u << (8 * left)) - 1u;
+                if (left) eq = eq && (lw[q] & m) == e[q];
+            }
+            if (eq) h |= 1u << j;
+        }
+        i = k + 1u;
+        if (i < end) {
+            if (rbyte(i) != ',') return 0;
+            i++;
+            if (i == end) return 0;  // "[1,]"
+        }
+    }
+    *hits = h;
+    return 1;
+}
+
 // Stage B for one request: patterns on the captured values, bitmap, fold.
 // res(p) values are V_T / V_F / V_E / V_U.
 // (s0, sstep: the selectors s0, s0 + sstep, ... only — the lanes of a wave sharing one
 // request's stage B; their t / u OR together)
+// (ring: the lane's 128-byte ring when the kernel has one free (the lean kernel's), for
+// incl_hits_ring; nullptr: arrays are walked in memory)
 AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef row, uint64_t t[2],
-                              uint64_t u[2], const uint64_t* dec = nullptr, uint32_t s0 = 0, uint32_t sstep = 1) {
+                              uint64_t u[2], const uint64_t* dec = nullptr, uint32_t s0 = 0, uint32_t sstep = 1,
+                              uint8_t* ring = nullptr) {
     // selector by selector: each captured value is decoded once for all its patterns;
     // when its String() is a byte span or a literal, eq/neq compare a dword at a time,
     // `matches` runs the DFA straight over the span and incl/excl walk a compact array
@@ -1111,7 +1206,8 @@ AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef ro
         const RawVal rv = raw_value(doc, v);
         const uint32_t begin = sps[s].begin;
         uint32_t hits = 0;
-        const bool fast_incl = cnt <= 32 && incl_hits(doc, v, pats, plist, begin, cnt, lits, &hits);
+        const bool fast_incl = cnt <= 32 && ((ring && incl_hits_ring(doc, v, pats, plist, begin, cnt, lits, ring, &hits)) ||
+                                             incl_hits(doc, v, pats, plist, begin, cnt, lits, &hits));
         for (uint32_t j = 0; j < cnt; j++) {
             const uint32_t p = plist[begin + j];
             const Pattern pt = pats[p];

@@ -115,10 +115,10 @@ __device__ __forceinline__ void fold_outputs(uint32_t r, const uint8_t* blob, co
 __device__ __forceinline__ bool finish_request(uint32_t r, const uint8_t* blob, const uint8_t* d, RowRef row,
                                                uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err,
                                                uint64_t* __restrict__ out_bm, uint32_t stride,
-                                               const uint64_t* dec = nullptr) {
+                                               const uint64_t* dec = nullptr, uint8_t* ring = nullptr) {
     const RulesetHdr* h = reinterpret_cast<const RulesetHdr*>(blob);
     uint64_t t[2], u[2];
-    patterns_from_row(blob, d, row, t, u, dec);
+    patterns_from_row(blob, d, row, t, u, dec, 0, 1, ring);
     if ((u[0] & ~h->unsupported[0]) | (u[1] & ~h->unsupported[1])) return false;
     if (out_bm) {
         uint64_t* orow = out_bm + (size_t)r * stride;

@@ -63,7 +63,8 @@ __global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_le
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
-    if (!finish_request(o, blob, d, row, out_tri, out_err, out_bm, stride, dec)) {
+    // (stage B's arrays are parsed from a copy in the lane's ring: scan_doc left no load in flight)
+    if (!finish_request(o, blob, d, row, out_tri, out_err, out_bm, stride, dec, wring + (threadIdx.x & 63u) * 16u)) {
         row[0] = kRowSlow;
         slow_ids[atomicAdd(slow_count, 1u)] = r;
     }
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
                 const uint32_t mis = (uint32_t)((uintptr_t)d & 15u);
                 lean::DmaLoader ld{reinterpret_cast<const uint4*>(d - mis), (len + mis + 15u) / 16u, wring};
                 ok = lean::scan_doc(blob, len, mis, row, wring + lane * 16u, ld, dec, 0u) &&
-                     finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec);
+                     finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec, wring + lane * 16u);
             }
             if (!ok) {
                 row[0] = kRowSlow;

@@ -316,7 +316,7 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
     if (!ok) return -1;
     if (row_out) std::memcpy(row_out, row.data(), row.size() * sizeof(uint64_t));
     uint64_t t[2], u[2];
-    patterns_from_row(blob, d, row.data(), t, u, dec);
+    patterns_from_row(blob, d, row.data(), t, u, dec, 0, 1, ld.lane_ring);  // (arrays from the ring, as the kernel)
     if ((u[0] & ~hd->unsupported[0]) | (u[1] & ~hd->unsupported[1])) return -1;
     const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
     for (uint32_t p = 0; p < hd->n_patterns; p++) {

@@ -295,3 +295,41 @@ def test_lean_colliding_long_keys(klen):
             n += 1
             assert lres == ot and tl == t_or, (klen, pad, mis, d)
     assert n == 70 * 16
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_stage_b_arrays_from_the_ring(seed):
+    """Stage B's incl / excl walk of an array copied into the lane's ring (incl_hits_ring):
+    arrays of unescaped strings of 0..17 bytes whose aligned blocks number 7..9 around the
+    ring's eight (every misalignment), with an escaped, numeric, nested or trailing-comma
+    element now and then (the memory walk decides those); the oracle's results."""
+    rng = np.random.default_rng(900 + seed)
+    words = ["", "a", "users", "reader", "x" * 8, "y" * 9, "z" * 15, "w" * 16, "v" * 17]
+    n = 0
+    for _ in range(60):
+        elems = []
+        target = int(rng.integers(90, 135))
+        while len("[" + ",".join(elems) + "]") < target:
+            elems.append(json.dumps(words[rng.integers(0, len(words))]))
+        r = rng.random()
+        if r < 0.1:
+            elems.insert(int(rng.integers(0, len(elems) + 1)), '"a\\"b"')
+        elif r < 0.2:
+            elems.insert(int(rng.integers(0, len(elems) + 1)), "12")
+        elif r < 0.25:
+            elems.insert(int(rng.integers(0, len(elems) + 1)), '["users"]')
+        arr = "[" + ",".join(elems) + "]"
+        d = ('{"s":"%s","g":%s,"t":"x"}' % ("p" * int(rng.integers(0, 40)), arr)).encode()
+        pats = [("g", int(rng.integers(3, 5)), words[rng.integers(0, len(words))]) for _ in range(3)]
+        pats.append(("g", 3, json.loads(elems[-1]) if elems[-1].startswith('"') else "12"))
+        nodes, root = _chain(len(pats))
+        rs = O.Ruleset(pats, nodes, root)
+        hr = H.HostRuleset(pats, nodes, root)
+        ot = [rs.pattern(p, d) for p in range(len(pats))]
+        t_or, _ = rs.matches(d)
+        for mis in range(16):
+            t, _, res, _ = H.eval_lean(hr, d, mis=mis)
+            if t >= 0 and 3 not in res:
+                n += 1
+                assert res == ot and t == t_or, (pats, d, mis)
+    assert n >= 60 * 16 * 0.8
