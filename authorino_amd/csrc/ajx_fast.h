@@ -1070,104 +1070,58 @@ AJX_HD bool incl_hits(const uint8_t* doc, const ValueRef& v, const Pattern* pats
     return true;
 }
 
-// incl_hits on a copy of the array in the lane's 128-byte ring (the lean kernel's, free
-// once stage A is done; chunk-major: ring byte x at (x >> 4) * 1024 + (x & 15)). The array's
-// aligned 16-byte blocks (at most eight) are loaded together and stored to the ring, so the
-// element walk reads LDS: one memory latency per array instead of one per dependent read
-// (about five per element in incl_hits). Compact arrays of unescaped strings of at most 16
-// bytes only; 1: *hits as incl_hits gives it, 0: not handled here (the caller takes
-// incl_hits, which decides every other array the same way it always did).
-AJX_HD uint32_t incl_hits_ring(const uint8_t* doc, const ValueRef& v, const Pattern* pats, const uint16_t* plist,
-                               uint32_t begin, uint32_t cnt, const uint8_t* lits, uint8_t* ring, uint32_t* hits) {
-    if (v.type != T_JSON || v.end - v.start < 2) return 0;
-    const uint32_t mis = (uint32_t)((uintptr_t)(doc + v.start) & 15u);
-    const uint32_t nb = (mis + (v.end - v.start) + 15u) / 16u;
-    if (nb > 8) return 0;
-    {
+// Stage B's values from LDS. In the lean kernel each lane's 128-byte share of the wave's
+// ring is free once stage A is done (and no load of it is in flight), so stage B copies a
+// captured value of up to kSpanMax bytes there and reads it from LDS: the value's aligned
+// 16-byte blocks (at most eight) are loaded together, one memory latency per value, where
+// walking it in memory costs one latency per dependent read (an array: about five per
+// element; an escaped string: one per byte; a short literal compare: one per byte). The
+// copy is contiguous, lane l's at l * kSpanStride in the wave's ring: 29 dwords, an odd
+// count, so the lanes' reads at one offset fall in different banks.
+constexpr uint32_t kSpanStride = 116;
+constexpr uint32_t kSpanMax = 112;
+// copy doc bytes [a, a + n) to buf (4-byte aligned): returns the offset in buf of byte a
+// (a's offset in its dword; the dwords that hold the span are copied whole), or ~0u when
+// they do not fit (more than kSpanStride bytes, or more than eight 16-byte blocks)
+AJX_HD uint32_t stage_span(const uint8_t* src, uint32_t n, uint8_t* buf) {
+    const uint32_t m16 = (uint32_t)((uintptr_t)src & 15u), sh = m16 & 3u;
+    const uint32_t nb = (m16 + n + 15u) / 16u, nd = (sh + n + 3u) / 4u;
+    if (nb > 8 || nd * 4u > kSpanStride || n == 0) return ~0u;
 #if defined(__HIPCC__)
-        using V16 = uint4;
+    using V16 = uint4;
 #else
-        using V16 = Block16;
+    using V16 = Block16;
 #endif
-        const V16* a4 = reinterpret_cast<const V16*>(doc + v.start - mis);
-        V16 blk[8];
+    const V16* a4 = reinterpret_cast<const V16*>(src - m16);
+    V16 blk[8];
 #pragma unroll
-        for (uint32_t j = 0; j < 8; j++) blk[j] = a4[j < nb ? j : nb - 1u];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) *reinterpret_cast<V16*>(ring + j * 1024u) = blk[j];
-    }
-    auto rw = [&](uint32_t q) -> uint32_t {  // the aligned dword at ring offset q (garbage past 127)
-        q &= 127u;
-        return *reinterpret_cast<const uint32_t*>(ring + (((q & 0x70u) << 6) | (q & 15u)));
-    };
-    auto r32 = [&](uint32_t a) -> uint32_t {  // 4 bytes from ring offset a
-        const uint32_t q = a & ~3u, sh = a & 3u;
-        const uint32_t w0 = rw(q), w1 = rw(q + 4u);
-#if defined(__HIP_DEVICE_COMPILE__)
-        return __builtin_amdgcn_alignbyte(w1, w0, sh);
-#else
-        return sh ? (w0 >> (8 * sh)) | (w1 << (32 - 8 * sh)) : w0;
+    for (uint32_t j = 0; j < 8; j++) blk[j] = a4[j < nb ? j : nb - 1u];
+    // dword k of block j is the span's dword 4 j + k - m16 / 4
+    uint32_t* bw = reinterpret_cast<uint32_t*>(buf);
+#if !defined(__HIPCC__)
+    // (host test builds: the bytes around the copy are poison, so that a read outside the
+    // value's span shows as a wrong answer against the oracle)
+    for (uint32_t k = 0; k < kSpanStride; k++) buf[k] = (k & 1u) ? 0x5Cu : 0x22u;
 #endif
-    };
-    auto rbyte = [&](uint32_t a) -> uint32_t { return rw(a & ~3u) >> (8 * (a & 3u)) & 0xFFu; };
-    const uint32_t end = mis + (v.end - v.start) - 1u;  // the ']' (ring offset)
-    if (rbyte(mis) != '[' || rbyte(end) != ']') return 0;
-    uint32_t h = 0, i = mis + 1u;
-    while (i < end) {
-        if (rbyte(i) != '"') return 0;  // (other elements: incl_hits)
-        uint32_t k = i + 1u;
-        for (;;) {  // the closing quote: the first '"' or '\\' after i
-            if (k >= end) return 0;
-            const uint32_t w = r32(k);
-            const uint32_t m = end - k >= 4 ? 0xFFFFFFFFu : (1u << (8 * (end - k))) - 1u;
-            const uint32_t f = (eq_bytes(w, 0x22222222u) | eq_bytes(w, 0x5C5C5C5Cu)) & m;
-            if (f) {
-                k += (uint32_t)__builtin_ctz(f) >> 3;
-                break;
-            }
-            k += 4;
-        }
-        if (rbyte(k) != '"') return 0;  // an escape
-        const uint32_t n = k - i - 1u;
-        if (n > 16) return 0;
-        // the element's bytes [i + 1, k) as four masked dwords
-        uint32_t e[4];
+    const int32_t d0 = -(int32_t)(m16 >> 2);
 #pragma unroll
-        for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t left = n > 4 * q ? n - 4 * q : 0u;
-            const uint32_t m = left >= 4 ? 0xFFFFFFFFu : (1u << (8 * left)) - 1u;
-            e[q] = left ? r32(i + 1u + 4 * q) & m : 0u;
-        }
-        for (uint32_t j = 0; j < cnt; j++) {
-            const Pattern pt = pats[plist[begin + j]];
-            if ((pt.op != OP_INCL && pt.op != OP_EXCL) || pt.state != P_OK || pt.lit_len != n) continue;
-            const uint32_t* lw = reinterpret_cast<const uint32_t*>(lits + pt.lit_off);  // (4-byte aligned)
-            bool eq = true;
+    for (uint32_t j = 0; j < 8; j++) {
+        const uint32_t x[4] = {blk[j].x, blk[j].y, blk[j].z, blk[j].w};
 #pragma unroll
-            for (uint32_t q = 0; q < 4; q++) {
-                const uint32_t left = n > 4 * q ? n - 4 * q : 0u;
-                const uint32_t m = left >= 4 ? 0xFFFFFFFFu : (1u << (8 * left)) - 1u;
-                if (left) eq = eq && (lw[q] & m) == e[q];
-            }
-            if (eq) h |= 1u << j;
-        }
-        i = k + 1u;
-        if (i < end) {
-            if (rbyte(i) != ',') return 0;
-            i++;
-            if (i == end) return 0;  // "[1,]"
+        for (uint32_t k = 0; k < 4; k++) {
+            const int32_t d = d0 + (int32_t)(4 * j + k);
+            if (d >= 0 && d < (int32_t)nd) bw[d] = x[k];
         }
     }
-    *hits = h;
-    return 1;
+    return sh;
 }
 
 // Stage B for one request: patterns on the captured values, bitmap, fold.
 // res(p) values are V_T / V_F / V_E / V_U.
 // (s0, sstep: the selectors s0, s0 + sstep, ... only — the lanes of a wave sharing one
 // request's stage B; their t / u OR together)
-// (ring: the lane's 128-byte ring when the kernel has one free (the lean kernel's), for
-// incl_hits_ring; nullptr: arrays are walked in memory)
+// (ring: the lane's span buffer when the kernel has one free (the lean kernel's, see
+// stage_span); nullptr: values are read in memory)
 AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef row, uint64_t t[2],
                               uint64_t u[2], const uint64_t* dec = nullptr, uint32_t s0 = 0, uint32_t sstep = 1,
                               uint8_t* ring = nullptr) {
@@ -1184,6 +1138,10 @@ AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef ro
     uint64_t t0 = 0, t1 = 0, u0 = h->unsupported[0], u1 = h->unsupported[1];
     const uint64_t nt0 = h->null_true[0], nt1 = h->null_true[1];
     const uint32_t ns = h->n_selectors;
+    // first the selectors decided without their record, then the others (needm) in order,
+    // each one's record loaded while the one before it is decided (a row read is a memory
+    // latency; `found` is one word, so selectors are < 64)
+    uint64_t needm = 0;
     for (uint32_t s = s0; s < ns; s += sstep) {
         const uint32_t cnt = sps[s].count;
         if (!cnt) continue;
@@ -1196,18 +1154,35 @@ AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef ro
             t0 |= sps[s].mask[0] & dec[1];
             continue;
         }
-        const uint64_t rec = row[1 + s];
+        needm |= 1ull << s;
+    }
+    uint64_t rec_next = needm ? row[1 + ctz64f(needm)] : 0ull;
+    while (needm) {
+        const uint32_t s = ctz64f(needm);
+        needm &= needm - 1ull;
+        const uint64_t rec = rec_next;
+        if (needm) rec_next = row[1 + ctz64f(needm)];
+        const uint32_t cnt = sps[s].count;
         const uint32_t meta = (uint32_t)(rec >> 32);
         ValueRef v;
         v.start = (uint32_t)rec;
         v.end = v.start + (meta & 0xFFFFFFu);
         v.type = (uint8_t)((meta >> 24) & 7u);
         v.esc = (uint8_t)((meta >> 27) & 1u);
-        const RawVal rv = raw_value(doc, v);
+        // (vd: where the value's bytes are read, the document or the lane's copy in LDS)
+        const uint8_t* vd = doc;
+        if (ring && v.end - v.start <= kSpanMax) {
+            const uint32_t at = stage_span(doc + v.start, v.end - v.start, ring);
+            if (at != ~0u) {
+                vd = ring;
+                v.end = at + (v.end - v.start);
+                v.start = at;
+            }
+        }
+        const RawVal rv = raw_value(vd, v);
         const uint32_t begin = sps[s].begin;
         uint32_t hits = 0;
-        const bool fast_incl = cnt <= 32 && ((ring && incl_hits_ring(doc, v, pats, plist, begin, cnt, lits, ring, &hits)) ||
-                                             incl_hits(doc, v, pats, plist, begin, cnt, lits, &hits));
+        const bool fast_incl = cnt <= 32 && incl_hits(vd, v, pats, plist, begin, cnt, lits, &hits);
         for (uint32_t j = 0; j < cnt; j++) {
             const uint32_t p = plist[begin + j];
             const Pattern pt = pats[p];
@@ -1217,15 +1192,15 @@ AJX_HD void patterns_from_row(const uint8_t* blob, const uint8_t* doc, RowRef ro
             } else if (pt.state != P_OK) {
                 r = pt.state == P_STATIC_E ? V_E : V_U;
             } else if (rv.ok && (pt.op == OP_EQ || pt.op == OP_NEQ)) {
-                r = raw_equals(doc, rv, pt, lits) == (pt.op == OP_EQ) ? V_T : V_F;
+                r = raw_equals(vd, rv, pt, lits) == (pt.op == OP_EQ) ? V_T : V_F;
             } else if (rv.ok && pt.op == OP_MATCHES) {
                 const bool m = rv.lit ? dfa_match_lit(blob, pt.dfa_off, rv.lit)
-                                      : dfa_match_span(blob, pt.dfa_off, doc + rv.a, rv.n);
+                                      : dfa_match_span(blob, pt.dfa_off, vd + rv.a, rv.n);
                 r = m ? V_T : V_F;
             } else if (fast_incl && (pt.op == OP_INCL || pt.op == OP_EXCL)) {
                 r = (((hits >> j) & 1u) != 0) == (pt.op == OP_INCL) ? V_T : V_F;
             } else {
-                r = eval_pattern(blob, pt, doc, v);
+                r = eval_pattern(blob, pt, vd, v);
             }
             const uint64_t bit = 1ull << (p & 63);
             if (r == V_T) {

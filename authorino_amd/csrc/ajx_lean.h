@@ -653,7 +653,7 @@ AJX_HD bool scan_doc(const uint8_t* blob, uint32_t n, uint32_t mis, RowRef row, 
         return true;
     }
     // (a walk that ended early may leave the next window's loads in flight: none may land in
-    // the ring after this, stage B copies arrays there)
+    // the ring after this, stage B copies values there)
     ld.template wait<0>();
     if (w.st != S_DONE || cr.bad <= (int32_t)w.pend) {  // (pend: the root's close)
         row[0] = kRowSlow;

@@ -9,6 +9,7 @@
 
 namespace ajx {
 
+static_assert(64 * kSpanStride <= lean::kRingBytesPerWave, "stage B's span buffers lie in the wave's ring");
 constexpr uint32_t kLeanMaxBlock = 1024;
 #ifndef AJX_LEAN_MAXBLOCK
 #define AJX_LEAN_MAXBLOCK kLeanMaxBlock
@@ -63,8 +64,9 @@ __global__ __launch_bounds__(AJX_LEAN_MAXBLOCK, AJX_LEAN_WAVES) void ajx_scan_le
         slow_ids[atomicAdd(slow_count, 1u)] = r;
         return;
     }
-    // (stage B's arrays are parsed from a copy in the lane's ring: scan_doc left no load in flight)
-    if (!finish_request(o, blob, d, row, out_tri, out_err, out_bm, stride, dec, wring + (threadIdx.x & 63u) * 16u)) {
+    // (stage B reads short values from a copy in the lane's share of the ring, stage_span:
+    // scan_doc left no load in flight)
+    if (!finish_request(o, blob, d, row, out_tri, out_err, out_bm, stride, dec, wring + (threadIdx.x & 63u) * kSpanStride)) {
         row[0] = kRowSlow;
         slow_ids[atomicAdd(slow_count, 1u)] = r;
     }
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(kFastBlock, AJX_FAST_WAVES) void ajx_scan_fused_ten
                 const uint32_t mis = (uint32_t)((uintptr_t)d & 15u);
                 lean::DmaLoader ld{reinterpret_cast<const uint4*>(d - mis), (len + mis + 15u) / 16u, wring};
                 ok = lean::scan_doc(blob, len, mis, row, wring + lane * 16u, ld, dec, 0u) &&
-                     finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec, wring + lane * 16u);
+                     finish_request(r, blob, d, row, out_tri, out_err, out_bm, stride, dec, wring + lane * kSpanStride);
             }
             if (!ok) {
                 row[0] = kRowSlow;
