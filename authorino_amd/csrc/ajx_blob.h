@@ -225,6 +225,10 @@ constexpr uint32_t kFlagFastOk = 4;
 constexpr uint32_t kLeanArr = 1, kLeanCaps = 2;
 
 constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the exact scan's buffers
+// the fold code is one flat All / Any of patterns 0..n_patterns - 1 in order (n_patterns
+// <= 64, one tree): its result is the first pattern, in index order, that is not the
+// group's identity (fold_outputs reads it off the bitmaps, no code interpreted)
+constexpr uint32_t kFlagFlatFold = 16;
 
 // Patterns the lean scan decides while it captures (ajx_lean.h): per selector, its first
 // two patterns (index < 64) that compare an unescaped string value's text with a literal

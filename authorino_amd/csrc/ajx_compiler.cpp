@@ -1099,6 +1099,12 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
     hdr.n_components = (uint32_t)comps.size();
     // (KeySlot::key_off8 reaches 512 KiB of literal pool)
     if (lits.size() >= 8u * 65536u) flags &= ~kFlagFastOk;
+    if (!forest && roots.size() == 1 && np >= 1 && np <= 64 && code.size() == np + 2u &&
+        ((code[0] >> 24) == C_OPEN_AND || (code[0] >> 24) == C_OPEN_OR) && (code[np + 1] >> 24) == C_CLOSE) {
+        bool flat = true;
+        for (uint32_t k = 0; k < np; k++) flat = flat && code[1 + k] == ((uint32_t)C_PAT << 24 | k);
+        if (flat) flags |= kFlagFlatFold;
+    }
     hdr.flags = flags;
     hdr.lean_feat = lean_feat;
     std::memcpy(b.blob.data(), &hdr, sizeof hdr);

@@ -1070,6 +1070,24 @@ AJX_HD bool incl_hits(const uint8_t* doc, const ValueRef& v, const Pattern* pats
     return true;
 }
 
+// The fold of a ruleset flagged kFlagFlatFold (one flat All / Any of patterns 0..n - 1 in
+// order, n <= 64): the first pattern that is not the group's identity decides, read off the
+// bitmaps (run_fold_bits' result, without interpreting the code)
+AJX_HD uint8_t flat_fold(const RulesetHdr* h, const uint32_t* code, const uint64_t t[2], const uint64_t u[2],
+                         const uint64_t se[2], int32_t* ep) {
+    const bool any = (code[0] >> 24) == C_OPEN_OR;
+    const uint32_t np = h->n_patterns;
+    const uint64_t pm = np >= 64 ? ~0ull : (1ull << np) - 1ull;
+    const uint64_t stick = pm & (se[0] | u[0] | (any ? t[0] : ~t[0]));  // (E and U are never the identity)
+    *ep = -1;
+    if (!stick) return any ? (uint8_t)V_F : (uint8_t)V_T;
+    const uint32_t k = (uint32_t)__builtin_ctzll(stick);
+    const uint8_t v = ((se[0] >> k) & 1u) ? (uint8_t)V_E : ((u[0] >> k) & 1u) ? (uint8_t)V_U
+                    : ((t[0] >> k) & 1u) ? (uint8_t)V_T : (uint8_t)V_F;
+    if (v == V_E || v == V_U) *ep = (int32_t)k;
+    return v;
+}
+
 // Stage B's values from LDS. In the lean kernel each lane's 128-byte share of the wave's
 // ring is free once stage A is done (and no load of it is in flight), so stage B copies a
 // captured value of up to kSpanMax bytes there and reads it from LDS: the value's aligned

@@ -95,6 +95,12 @@ __device__ __forceinline__ void fold_outputs(uint32_t r, const uint8_t* blob, co
                                              uint8_t* __restrict__ out_tri, int32_t* __restrict__ out_err) {
     const uint32_t* code = reinterpret_cast<const uint32_t*>(blob + h->off_code);
     const uint32_t nt = h->pad1[0];
+    if (h->flags & kFlagFlatFold) {  // (one tree, [open, pattern 0, ..., pattern n - 1, close])
+        int32_t ep;
+        out_tri[r] = flat_fold(h, code, t, u, se, &ep);
+        if (out_err) out_err[r] = ep;
+        return;
+    }
     if (nt == 0) {
         int32_t ep;
         out_tri[r] = run_fold_bits(code, h->n_code, t, u, se, &ep);

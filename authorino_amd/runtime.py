@@ -90,7 +90,10 @@ def load_library(path: str = LIB_PATH):
         L = C.CDLL(path)
         L.authjx_build_hash.argtypes = []
         L.authjx_build_hash.restype = C.c_char_p
-        _check_build_hash(L, path)
+        # (a profiling build named by AUTHJX_LIB is a whole library of its own, possibly of
+        # an earlier tree for an A/B run: only the in-tree library must match the sources)
+        if not os.environ.get("AUTHJX_LIB"):
+            _check_build_hash(L, path)
         L.authjx_init.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         L.authjx_init.restype = C.c_int
         L.authjx_shutdown.argtypes = [C.c_void_p]

@@ -287,6 +287,8 @@ extern "C" void ht_lean_last_dec(uint64_t* out) {
 // default when no caller reads the rows); 1 every record
 static uint32_t g_lean_keep = 1;
 extern "C" void ht_lean_keep(int keep) { g_lean_keep = keep ? 1u : 0u; }
+static uint64_t g_flat_folds = 0;  // (lean evaluations whose ruleset took the flat fold)
+extern "C" uint64_t ht_flat_folds() { return g_flat_folds; }
 extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
                                 uint64_t* row_out) {
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
@@ -316,7 +318,7 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
     if (!ok) return -1;
     if (row_out) std::memcpy(row_out, row.data(), row.size() * sizeof(uint64_t));
     uint64_t t[2], u[2];
-    patterns_from_row(blob, d, row.data(), t, u, dec, 0, 1, ld.lane_ring);  // (arrays from the ring, as the kernel)
+    patterns_from_row(blob, d, row.data(), t, u, dec, 0, 1, ld.lane_ring);  // (values from the lane's buffer, as the kernel)
     if ((u[0] & ~hd->unsupported[0]) | (u[1] & ~hd->unsupported[1])) return -1;
     const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
     for (uint32_t p = 0; p < hd->n_patterns; p++) {
@@ -324,7 +326,15 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
         uint32_t k = p >> 6;
         res[p] = (hd->static_error[k] & bit) ? V_E : (u[k] & bit) ? V_U : (t[k] & bit) ? V_T : V_F;
     }
-    return run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
+    const int tri = run_fold(code, hd->n_code, [&](uint32_t p) { return res[p]; }, err);
+    if (hd->flags & kFlagFlatFold) {  // (the kernels' fold for such rulesets: it must agree)
+        const uint64_t se[2] = {hd->static_error[0], hd->static_error[1]};
+        int32_t fe;
+        const uint8_t ft = flat_fold(hd, code, t, u, se, &fe);
+        g_flat_folds++;
+        if (ft != tri || fe != *err) return 99;  // (no tri-state: the test's comparison fails)
+    }
+    return tri;
 }
 extern "C" int ht_eval_lean(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err) {
     return ht_eval_lean_row(h, doc, len, mis, res, err, nullptr);

@@ -333,3 +333,39 @@ def test_stage_b_arrays_from_the_ring(seed):
                 n += 1
                 assert res == ot and t == t_or, (pats, d, mis)
     assert n >= 60 * 16 * 0.8
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_flat_fold_agrees_with_the_code_interpreter(seed):
+    """Rulesets of one flat All / Any over patterns 0..n-1 (kFlagFlatFold: the kernels read
+    the fold off the bitmaps) on random documents: the host harness computes both folds and
+    returns no tri-state when they differ; the oracle's results. c2's ruleset is one."""
+    import ctypes as C
+
+    from authorino_amd import jsonexp as J
+    from authorino_amd import workloads as W
+
+    L = H.lib()
+    L.ht_flat_folds.restype = C.c_uint64
+    before = L.ht_flat_folds()
+    rng = np.random.default_rng(700 + seed)
+    n = 0
+    for _ in range(60):
+        pats = FU.rand_patterns(rng, int(rng.integers(1, 12)))
+        expr = (J.All if rng.random() < 0.5 else J.Any)(*[J.Pattern(s, J.Operator(op), v) for s, op, v in pats])
+        hr = H.HostRuleset.from_expression(expr)
+        rs = O.Ruleset.from_expression(expr)
+        for _ in range(10):
+            d = FU.rand_doc(rng, ws=False)
+            t_or, _ = rs.matches(d)
+            tl, _, _, _ = H.eval_lean(hr, d, mis=int(rng.integers(0, 16)))
+            if tl >= 0:
+                n += 1
+                assert tl == t_or, (pats, d)
+    w = W.make("c2", n=50, seed=3)
+    hr = H.HostRuleset.from_expression(w.expr)
+    rs = O.Ruleset.from_expression(w.expr)
+    for i in range(w.n):
+        tl, _, _, _ = H.eval_lean(hr, w.doc(i), mis=i & 15)
+        assert tl == rs.matches(w.doc(i))[0]
+    assert L.ht_flat_folds() - before >= w.n + n // 2  # (one-pattern trees compile without a group)
