@@ -218,6 +218,8 @@ struct RulesetHdr {
     uint64_t null_true[2];      // pattern p is T when its selector finds nothing (Null)
     uint64_t static_error[2];   // pattern p is a static E
     uint64_t unsupported[2];    // pattern p can not be decided on the device
+    // kFlagGroupFold: {patterns in Any groups, patterns in groups, each group's first pattern}
+    uint64_t fold_grp[3];
 };
 constexpr uint32_t kFlagFastOk = 4;
 // RulesetHdr::lean_feat: some trie node has array-index children (the lean walk enters
@@ -229,6 +231,11 @@ constexpr uint32_t kFlagBufs = 8;  // a selector builds a text (a '#' list): the
 // <= 64, one tree): its result is the first pattern, in index order, that is not the
 // group's identity (fold_outputs reads it off the bitmaps, no code interpreted)
 constexpr uint32_t kFlagFlatFold = 16;
+// the fold code is one All / Any whose children are patterns and groups of the other kind
+// over patterns only, patterns 0..n_patterns - 1 in code order (n_patterns <= 64, one
+// tree; c3's All(Any x4, All x4) flattens to one): group_fold reads it off the bitmaps,
+// one step per group, with the group layout in RulesetHdr::fold_grp
+constexpr uint32_t kFlagGroupFold = 32;
 
 // Patterns the lean scan decides while it captures (ajx_lean.h): per selector, its first
 // two patterns (index < 64) that compare an unescaped string value's text with a literal

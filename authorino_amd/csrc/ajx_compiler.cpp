@@ -1105,6 +1105,45 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         for (uint32_t k = 0; k < np; k++) flat = flat && code[1 + k] == ((uint32_t)C_PAT << 24 | k);
         if (flat) flags |= kFlagFlatFold;
     }
+    if (!forest && roots.size() == 1 && np >= 1 && np <= 64 && !(flags & kFlagFlatFold) && code.size() >= 3 &&
+        ((code[0] >> 24) == C_OPEN_AND || (code[0] >> 24) == C_OPEN_OR) && (code.back() >> 24) == C_CLOSE) {
+        // [open X, (pattern | open Y, pattern+, close)*, close], Y != X, patterns in order
+        const uint32_t outer = code[0] >> 24, inner = outer == C_OPEN_AND ? C_OPEN_OR : C_OPEN_AND;
+        uint64_t g_any = 0, g_in = 0, g_start = 0;
+        uint32_t next = 0, k = 1;
+        bool ok = true;
+        const uint32_t last = (uint32_t)code.size() - 1;
+        while (ok && k < last) {
+            const uint32_t op = code[k] >> 24;
+            if (op == C_PAT && (code[k] & 0xFFFFFFu) == next) {
+                next++;
+                k++;
+            } else if (op == inner) {
+                const uint32_t lo = next;
+                k++;
+                while (k < last && (code[k] >> 24) == C_PAT && (code[k] & 0xFFFFFFu) == next) {
+                    next++;
+                    k++;
+                }
+                ok = next > lo && k < last && (code[k] >> 24) == C_CLOSE;
+                k++;
+                if (ok) {
+                    const uint64_t m = (next >= 64 ? ~0ull : (1ull << next) - 1ull) & ~((1ull << lo) - 1ull);
+                    g_in |= m;
+                    if (inner == C_OPEN_OR) g_any |= m;
+                    g_start |= 1ull << lo;
+                }
+            } else {
+                ok = false;
+            }
+        }
+        if (ok && k == last && next == np && g_start) {
+            flags |= kFlagGroupFold;
+            hdr.fold_grp[0] = g_any;
+            hdr.fold_grp[1] = g_in;
+            hdr.fold_grp[2] = g_start;
+        }
+    }
     hdr.flags = flags;
     hdr.lean_feat = lean_feat;
     std::memcpy(b.blob.data(), &hdr, sizeof hdr);

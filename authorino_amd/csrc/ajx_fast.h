@@ -1088,6 +1088,56 @@ AJX_HD uint8_t flat_fold(const RulesetHdr* h, const uint32_t* code, const uint64
     return v;
 }
 
+// The fold of a ruleset flagged kFlagGroupFold (one All / Any over patterns and groups of
+// the other kind, patterns 0..n - 1 in code order). A child decides the outer group when
+// its value is not the outer identity; a group's value is its first pattern that is not
+// the group's identity (or the identity when there is none). The lone patterns that
+// decide come off the bitmaps at once; the groups before the first of them are taken in
+// order, one bitmap step each (run_fold_bits' result, without interpreting the code).
+AJX_HD uint8_t group_fold(const RulesetHdr* h, const uint32_t* code, const uint64_t t[2], const uint64_t u[2],
+                          const uint64_t se[2], int32_t* ep) {
+    const bool any = (code[0] >> 24) == C_OPEN_OR;
+    const uint32_t np = h->n_patterns;
+    const uint64_t pm = np >= 64 ? ~0ull : (1ull << np) - 1ull;
+    const uint64_t g_any = h->fold_grp[0], g_in = h->fold_grp[1];
+    const uint64_t eu = se[0] | u[0], t0 = t[0];
+    const uint64_t lone = pm & ~g_in & (eu | (any ? t0 : ~t0));   // lone patterns that decide
+    const uint64_t inner = g_in & (eu | (g_any & t0) | (~g_any & ~t0));  // not their group's identity
+    const uint32_t kl = lone ? (uint32_t)__builtin_ctzll(lone) : 64u;
+    const uint8_t ident = any ? (uint8_t)V_F : (uint8_t)V_T;
+    auto value = [&](uint32_t k) -> uint8_t {
+        return ((se[0] >> k) & 1u) ? (uint8_t)V_E : ((u[0] >> k) & 1u) ? (uint8_t)V_U
+             : ((t0 >> k) & 1u) ? (uint8_t)V_T : (uint8_t)V_F;
+    };
+    *ep = -1;
+    uint64_t g = h->fold_grp[2];
+    while (g) {
+        const uint32_t lo = (uint32_t)__builtin_ctzll(g);
+        if (lo > kl) break;
+        g &= g - 1ull;
+        // the group runs to the next group's first pattern or the next lone pattern
+        const uint64_t above = lo >= 63 ? 0ull : ~0ull << (lo + 1);
+        const uint64_t ends = (g | ~g_in) & above;
+        const uint64_t range = (ends ? ((1ull << __builtin_ctzll(ends)) - 1ull) : ~0ull) & ~((1ull << lo) - 1ull);
+        const uint64_t s = inner & range;
+        if (!s) {  // the group's identity, the other kind's: it decides
+            const uint8_t v = ((g_any >> lo) & 1u) ? (uint8_t)V_F : (uint8_t)V_T;
+            if (v != ident) return v;
+            continue;
+        }
+        const uint32_t k = (uint32_t)__builtin_ctzll(s);
+        const uint8_t v = value(k);
+        if (v != ident) {
+            if (v == V_E || v == V_U) *ep = (int32_t)k;
+            return v;
+        }
+    }
+    if (kl == 64u) return ident;
+    const uint8_t v = value(kl);
+    if (v == V_E || v == V_U) *ep = (int32_t)kl;
+    return v;
+}
+
 // Stage B's values from LDS. In the lean kernel each lane's 128-byte share of the wave's
 // ring is free once stage A is done (and no load of it is in flight), so stage B copies a
 // captured value of up to kSpanMax bytes there and reads it from LDS: the value's aligned

@@ -101,6 +101,12 @@ __device__ __forceinline__ void fold_outputs(uint32_t r, const uint8_t* blob, co
         if (out_err) out_err[r] = ep;
         return;
     }
+    if (h->flags & kFlagGroupFold) {  // (one tree: groups of patterns under one All / Any)
+        int32_t ep;
+        out_tri[r] = group_fold(h, code, t, u, se, &ep);
+        if (out_err) out_err[r] = ep;
+        return;
+    }
     if (nt == 0) {
         int32_t ep;
         out_tri[r] = run_fold_bits(code, h->n_code, t, u, se, &ep);

@@ -289,6 +289,8 @@ static uint32_t g_lean_keep = 1;
 extern "C" void ht_lean_keep(int keep) { g_lean_keep = keep ? 1u : 0u; }
 static uint64_t g_flat_folds = 0;  // (lean evaluations whose ruleset took the flat fold)
 extern "C" uint64_t ht_flat_folds() { return g_flat_folds; }
+static uint64_t g_group_folds = 0;  // (the same for the group fold)
+extern "C" uint64_t ht_group_folds() { return g_group_folds; }
 extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err,
                                 uint64_t* row_out) {
     const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
@@ -334,7 +336,41 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
         g_flat_folds++;
         if (ft != tri || fe != *err) return 99;  // (no tri-state: the test's comparison fails)
     }
+    if (hd->flags & kFlagGroupFold) {
+        const uint64_t se[2] = {hd->static_error[0], hd->static_error[1]};
+        int32_t fe;
+        const uint8_t ft = group_fold(hd, code, t, u, se, &fe);
+        g_group_folds++;
+        if (ft != tri || fe != *err) return 99;
+    }
     return tri;
+}
+// group_fold against the code interpreter on n random (T, U, static E) bitmaps of the
+// ruleset's patterns: the number of differences (-1: the ruleset is not kFlagGroupFold)
+extern "C" int64_t ht_group_fold_check(void* h, uint64_t seed, uint32_t n) {
+    const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
+    const RulesetHdr* hd = (const RulesetHdr*)blob;
+    if (!(hd->flags & kFlagGroupFold)) return -1;
+    const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
+    uint64_t x = seed * 0x9E3779B97F4A7C15ull + 1ull;
+    auto rnd = [&]() {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        return x;
+    };
+    int64_t bad = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        // mostly-true T, sparse U and E (bits at 1/16 and 1/64 density), now and then dense
+        const uint64_t t[2] = {(i & 3) ? (rnd() | rnd() | rnd()) : rnd(), 0ull};
+        const uint64_t u[2] = {(i & 7) ? (rnd() & rnd() & rnd() & rnd()) : 0ull, 0ull};
+        const uint64_t se[2] = {(i & 5) ? (rnd() & rnd() & rnd() & rnd() & rnd() & rnd()) : 0ull, 0ull};
+        int32_t e1, e2;
+        const uint8_t a = run_fold_bits(code, hd->n_code, t, u, se, &e1);
+        const uint8_t b = group_fold(hd, code, t, u, se, &e2);
+        if (a != b || e1 != e2) bad++;
+    }
+    return bad;
 }
 extern "C" int ht_eval_lean(void* h, const uint8_t* doc, uint32_t len, uint32_t mis, uint8_t* res, int32_t* err) {
     return ht_eval_lean_row(h, doc, len, mis, res, err, nullptr);

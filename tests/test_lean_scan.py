@@ -369,3 +369,70 @@ def test_flat_fold_agrees_with_the_code_interpreter(seed):
         tl, _, _, _ = H.eval_lean(hr, w.doc(i), mis=i & 15)
         assert tl == rs.matches(w.doc(i))[0]
     assert L.ht_flat_folds() - before >= w.n + n // 2  # (one-pattern trees compile without a group)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_group_fold_agrees_with_the_code_interpreter(seed):
+    """Rulesets of one All / Any over lone patterns and groups of the other kind
+    (kFlagGroupFold: the kernels read the fold off the bitmaps, one step per group): the
+    harness's group_fold against the code interpreter on random T / U / static-E bitmaps
+    (E and U at every position, groups first, last, adjacent, of one to eight patterns), and
+    on random documents against the oracle. c3's ruleset is one."""
+    import ctypes as C
+
+    from authorino_amd import jsonexp as J
+    from authorino_amd import workloads as W
+
+    L = H.lib()
+    L.ht_group_folds.restype = C.c_uint64
+    L.ht_group_fold_check.restype = C.c_int64
+    L.ht_group_fold_check.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32]
+    before = L.ht_group_folds()
+    rng = np.random.default_rng(800 + seed)
+    n = n_group = 0
+    for it in range(60):
+        outer = J.All if rng.random() < 0.5 else J.Any
+        inner = J.Any if outer is J.All else J.All
+        kids = []
+        for _ in range(int(rng.integers(1, 7))):
+            if rng.random() < 0.5:
+                kids.append(None)
+            else:
+                kids.append(int(rng.integers(2, 9)))
+        if all(k is None for k in kids):
+            kids[int(rng.integers(0, len(kids)))] = int(rng.integers(2, 9))
+        npat = sum(1 if k is None else k for k in kids)
+        pats = FU.rand_patterns(rng, npat)
+        ps = [J.Pattern(s, J.Operator(op), v) for s, op, v in pats]
+        args, i = [], 0
+        for k in kids:
+            if k is None:
+                args.append(ps[i])
+                i += 1
+            else:
+                args.append(inner(*ps[i:i + k]))
+                i += k
+        expr = outer(*args)
+        hr = H.HostRuleset.from_expression(expr)
+        bad = L.ht_group_fold_check(hr._h, it + 1000 * seed, 4000)
+        if bad < 0:
+            continue  # (the compiler merged or reordered it: not a group fold)
+        n_group += 1
+        assert bad == 0, (kids, pats)
+        rs = O.Ruleset.from_expression(expr)
+        for _ in range(6):
+            d = FU.rand_doc(rng, ws=False)
+            t_or, _ = rs.matches(d)
+            tl, _, _, _ = H.eval_lean(hr, d, mis=int(rng.integers(0, 16)))
+            if tl >= 0:
+                n += 1
+                assert tl == t_or, (kids, pats, d)
+    assert n_group >= 40
+    w = W.make("c3", n=50, seed=3)
+    hr = H.HostRuleset.from_expression(w.expr)
+    assert L.ht_group_fold_check(hr._h, 7 + seed, 20000) == 0
+    rs = O.Ruleset.from_expression(w.expr)
+    for i in range(w.n):
+        tl, _, _, _ = H.eval_lean(hr, w.doc(i), mis=i & 15)
+        assert tl == rs.matches(w.doc(i))[0]
+    assert L.ht_group_folds() - before >= w.n + n // 2
