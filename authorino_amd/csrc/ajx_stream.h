@@ -1009,7 +1009,9 @@ AJX_HD bool finish_light(uint32_t r, const uint8_t* blob, const Tabs& T, const u
     const uint32_t nt = h->pad1[0];
     if (nt == 0) {
         int32_t ep;
-        out_tri[r] = run_fold_bits(code, h->n_code, t, u, se, &ep);
+        out_tri[r] = (h->flags & kFlagFlatFold)    ? flat_fold(h, code, t, u, se, &ep)
+                     : (h->flags & kFlagGroupFold) ? group_fold(h, code, t, u, se, &ep)
+                                                   : run_fold_bits(code, h->n_code, t, u, se, &ep);
         if (out_err) out_err[r] = ep;
         return true;
     }
@@ -1153,6 +1155,9 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
     // WAVE: every lane runs the (uniform) fold, its code words handed out from registers
     // (64 per coalesced read) instead of one dependent memory read each
     auto fold = [&](const uint32_t* c, uint32_t nc, int32_t* ep) -> uint8_t {
+        // (one tree whose fold reads off the bitmaps: kFlagFlatFold / kFlagGroupFold)
+        if (c == code && nt == 0 && (h->flags & kFlagGroupFold)) return group_fold(h, code, t, u, se, ep);
+        if (!WAVE && c == code && nt == 0 && (h->flags & kFlagFlatFold)) return flat_fold(h, code, t, u, se, ep);
         if constexpr (WAVE) {
             // a flat All / Any (open, patterns, close; up to 64 words): the lanes hold one
             // word each and the result is the first leaf, in code order, that is not the
