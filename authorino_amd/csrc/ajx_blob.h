@@ -236,6 +236,13 @@ constexpr uint32_t kFlagFlatFold = 16;
 // tree; c3's All(Any x4, All x4) flattens to one): group_fold reads it off the bitmaps,
 // one step per group, with the group layout in RulesetHdr::fold_grp
 constexpr uint32_t kFlagGroupFold = 32;
+// A forest's trees of the same shapes (RulesetHdr::pad1[2]: offset of TreeFold[n_trees], 0
+// when the forest has none): tree k's patterns base .. base + n - 1 in code order
+// (n <= 64), its fold read off those bits of the bitmaps; shape 0: the code is interpreted
+struct TreeFold {
+    uint32_t base, n, shape, any;  // shape 1: one flat All / Any or a two-level one
+    uint64_t g_any, g_in, g_start;  // as RulesetHdr::fold_grp, bit j = pattern base + j
+};
 
 // Patterns the lean scan decides while it captures (ajx_lean.h): per selector, its first
 // two patterns (index < 64) that compare an unescaped string value's text with a literal

@@ -392,6 +392,63 @@ struct Builder {
 }  // namespace
 
 namespace {
+// the shape of one tree's fold code that tree_fold reads off the bitmaps: [open X,
+// (pattern | open Y, pattern+, close)*, close], Y != X, pattern indices consecutive in code
+// order (base, base + 1, ...), at most 64 of them
+bool tree_fold_shape(const uint32_t* code, uint32_t n, TreeFold* f) {
+    if (n < 3 || (code[n - 1] >> 24) != C_CLOSE) return false;
+    const uint32_t outer = code[0] >> 24;
+    if (outer != C_OPEN_AND && outer != C_OPEN_OR) return false;
+    const uint32_t inner = outer == C_OPEN_AND ? C_OPEN_OR : C_OPEN_AND;
+    uint32_t base = ~0u, next = 0, k = 1;
+    uint64_t g_any = 0, g_in = 0, g_start = 0;
+    auto take = [&](uint32_t w) {  // the next pattern in order
+        const uint32_t p = w & 0xFFFFFFu;
+        if (base == ~0u) {
+            base = p;
+            next = p;
+        }
+        if (p != next || p - base >= 64) return false;
+        next++;
+        return true;
+    };
+    while (k < n - 1) {
+        const uint32_t op = code[k] >> 24;
+        if (op == C_PAT) {
+            if (!take(code[k])) return false;
+            k++;
+        } else if (op == inner) {
+            k++;
+            bool first = true;
+            uint32_t lo_rel = 0;
+            while (k < n - 1 && (code[k] >> 24) == C_PAT) {
+                if (!take(code[k])) return false;
+                if (first) lo_rel = (code[k] & 0xFFFFFFu) - base;
+                first = false;
+                k++;
+            }
+            if (first || k >= n - 1 || (code[k] >> 24) != C_CLOSE) return false;
+            k++;
+            const uint32_t hi_rel = next - base;
+            const uint64_t m = (hi_rel >= 64 ? ~0ull : (1ull << hi_rel) - 1ull) & ~((1ull << lo_rel) - 1ull);
+            g_in |= m;
+            if (inner == C_OPEN_OR) g_any |= m;
+            g_start |= 1ull << lo_rel;
+        } else {
+            return false;
+        }
+    }
+    if (base == ~0u || next > kFastMaxPatterns) return false;  // (the kernels' bitmaps are 128 bits)
+    f->base = base;
+    f->n = next - base;
+    f->shape = 1;
+    f->any = outer == C_OPEN_OR ? 1u : 0u;
+    f->g_any = g_any;
+    f->g_in = g_in;
+    f->g_start = g_start;
+    return true;
+}
+
 int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, bool forest, CompiledRuleset* out,
                  std::string* err, const std::vector<uint8_t>* kept = nullptr);
 }
@@ -1035,6 +1092,16 @@ int compile_core(const authjx_tree* tree, const std::vector<int32_t>& roots, boo
         hdr.pad1[0] = (uint32_t)roots.size();
         hdr.pad1[1] = (uint32_t)b.align16();
         b.append(root_code.data(), root_code.size() * sizeof(uint32_t));
+        std::vector<TreeFold> tf(roots.size());
+        bool any_tf = false;
+        for (size_t k = 0; k < roots.size(); k++) {
+            tf[k] = TreeFold{};
+            any_tf |= tree_fold_shape(code.data() + root_code[2 * k], root_code[2 * k + 1], &tf[k]);
+        }
+        if (any_tf) {
+            hdr.pad1[2] = (uint32_t)b.align16();
+            b.append(tf.data(), tf.size() * sizeof(TreeFold));
+        }
     }
     hdr.off_literals = (uint32_t)b.align16();
     lits.append(16, '\0');  // dword reads past a literal's end stay inside the pool

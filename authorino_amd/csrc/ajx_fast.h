@@ -1094,13 +1094,13 @@ AJX_HD uint8_t flat_fold(const RulesetHdr* h, const uint32_t* code, const uint64
 // the group's identity (or the identity when there is none). The lone patterns that
 // decide come off the bitmaps at once; the groups before the first of them are taken in
 // order, one bitmap step each (run_fold_bits' result, without interpreting the code).
-AJX_HD uint8_t group_fold(const RulesetHdr* h, const uint32_t* code, const uint64_t t[2], const uint64_t u[2],
-                          const uint64_t se[2], int32_t* ep) {
-    const bool any = (code[0] >> 24) == C_OPEN_OR;
-    const uint32_t np = h->n_patterns;
+// (fold_masks: patterns 0..np - 1 of one tree's own bitmaps t0 / u0 / s0 and its group
+// masks; *ep is the tree's pattern, from 0)
+AJX_HD uint8_t fold_masks(bool any, uint32_t np, uint64_t g_any, uint64_t g_in, uint64_t g_start, uint64_t t0,
+                          uint64_t u0, uint64_t s0, int32_t* ep) {
     const uint64_t pm = np >= 64 ? ~0ull : (1ull << np) - 1ull;
-    const uint64_t g_any = h->fold_grp[0], g_in = h->fold_grp[1];
-    const uint64_t eu = se[0] | u[0], t0 = t[0];
+    const uint64_t se[1] = {s0}, u[1] = {u0};
+    const uint64_t eu = s0 | u0;
     const uint64_t lone = pm & ~g_in & (eu | (any ? t0 : ~t0));   // lone patterns that decide
     const uint64_t inner = g_in & (eu | (g_any & t0) | (~g_any & ~t0));  // not their group's identity
     const uint32_t kl = lone ? (uint32_t)__builtin_ctzll(lone) : 64u;
@@ -1110,7 +1110,7 @@ AJX_HD uint8_t group_fold(const RulesetHdr* h, const uint32_t* code, const uint6
              : ((t0 >> k) & 1u) ? (uint8_t)V_T : (uint8_t)V_F;
     };
     *ep = -1;
-    uint64_t g = h->fold_grp[2];
+    uint64_t g = g_start;
     while (g) {
         const uint32_t lo = (uint32_t)__builtin_ctzll(g);
         if (lo > kl) break;
@@ -1135,6 +1135,24 @@ AJX_HD uint8_t group_fold(const RulesetHdr* h, const uint32_t* code, const uint6
     if (kl == 64u) return ident;
     const uint8_t v = value(kl);
     if (v == V_E || v == V_U) *ep = (int32_t)kl;
+    return v;
+}
+AJX_HD uint8_t group_fold(const RulesetHdr* h, const uint32_t* code, const uint64_t t[2], const uint64_t u[2],
+                          const uint64_t se[2], int32_t* ep) {
+    return fold_masks((code[0] >> 24) == C_OPEN_OR, h->n_patterns, h->fold_grp[0], h->fold_grp[1], h->fold_grp[2],
+                      t[0], u[0], se[0], ep);
+}
+// bits base .. base + n - 1 of a 128-bit bitmap (n <= 64, base + n <= 128)
+AJX_HD uint64_t bits_at(const uint64_t w[2], uint32_t base, uint32_t n) {
+    const uint64_t lo = base >= 64 ? w[1] >> (base - 64u) : base ? (w[0] >> base) | (w[1] << (64u - base)) : w[0];
+    return n >= 64 ? lo : lo & ((1ull << n) - 1ull);
+}
+// a forest's tree with a TreeFold shape: its fold off its own bits of the bitmaps
+AJX_HD uint8_t tree_fold(const TreeFold& f, const uint64_t t[2], const uint64_t u[2], const uint64_t se[2],
+                         int32_t* ep) {
+    const uint8_t v = fold_masks(f.any != 0, f.n, f.g_any, f.g_in, f.g_start, bits_at(t, f.base, f.n),
+                                 bits_at(u, f.base, f.n), bits_at(se, f.base, f.n), ep);
+    if (*ep >= 0) *ep += (int32_t)f.base;
     return v;
 }
 

@@ -114,9 +114,11 @@ __device__ __forceinline__ void fold_outputs(uint32_t r, const uint8_t* blob, co
         return;
     }
     const uint32_t* rc = reinterpret_cast<const uint32_t*>(blob + h->pad1[1]);
+    const TreeFold* tf = h->pad1[2] ? reinterpret_cast<const TreeFold*>(blob + h->pad1[2]) : nullptr;
     for (uint32_t k = 0; k < nt; k++) {
         int32_t ep;
-        out_tri[(size_t)r * nt + k] = run_fold_bits(code + rc[2 * k], rc[2 * k + 1], t, u, se, &ep);
+        out_tri[(size_t)r * nt + k] = tf && tf[k].shape ? tree_fold(tf[k], t, u, se, &ep)
+                                                        : run_fold_bits(code + rc[2 * k], rc[2 * k + 1], t, u, se, &ep);
         if (out_err) out_err[(size_t)r * nt + k] = ep;
     }
 }

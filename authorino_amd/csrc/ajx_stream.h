@@ -1016,9 +1016,11 @@ AJX_HD bool finish_light(uint32_t r, const uint8_t* blob, const Tabs& T, const u
         return true;
     }
     const uint32_t* rc = reinterpret_cast<const uint32_t*>(blob + h->pad1[1]);
+    const TreeFold* tf = h->pad1[2] ? reinterpret_cast<const TreeFold*>(blob + h->pad1[2]) : nullptr;
     for (uint32_t k = 0; k < nt; k++) {
         int32_t ep;
-        out_tri[(size_t)r * nt + k] = run_fold_bits(code + rc[2 * k], rc[2 * k + 1], t, u, se, &ep);
+        out_tri[(size_t)r * nt + k] = tf && tf[k].shape ? tree_fold(tf[k], t, u, se, &ep)
+                                                        : run_fold_bits(code + rc[2 * k], rc[2 * k + 1], t, u, se, &ep);
         if (out_err) out_err[(size_t)r * nt + k] = ep;
     }
     return true;
@@ -1210,9 +1212,10 @@ AJX_HD bool finish_full(uint32_t r, const uint8_t* blob, const uint8_t* d, uint3
         return true;
     }
     const uint32_t* rc = reinterpret_cast<const uint32_t*>(blob + h->pad1[1]);
+    const TreeFold* tf = h->pad1[2] ? reinterpret_cast<const TreeFold*>(blob + h->pad1[2]) : nullptr;
     for (uint32_t k = 0; k < nt; k++) {
         int32_t ep;
-        const uint8_t v = fold(code + rc[2 * k], rc[2 * k + 1], &ep);
+        const uint8_t v = tf && tf[k].shape ? tree_fold(tf[k], t, u, se, &ep) : fold(code + rc[2 * k], rc[2 * k + 1], &ep);
         if (lane == 0) {
             out_tri[(size_t)r * nt + k] = v;
             if (out_err) out_err[(size_t)r * nt + k] = ep;

@@ -345,6 +345,41 @@ extern "C" int ht_eval_lean_row(void* h, const uint8_t* doc, uint32_t len, uint3
     }
     return tri;
 }
+// tree_fold against the code interpreter for every forest tree with a TreeFold shape, on n
+// random 128-bit (T, U, static E) bitmaps: the number of differences (-1: no such tree)
+extern "C" int64_t ht_tree_fold_check(void* h, uint64_t seed, uint32_t n) {
+    const uint8_t* blob = ((HtRuleset*)h)->c.blob.data();
+    const RulesetHdr* hd = (const RulesetHdr*)blob;
+    const uint32_t nt = hd->pad1[0];
+    if (!nt || !hd->pad1[2]) return -1;
+    const uint32_t* code = (const uint32_t*)(blob + hd->off_code);
+    const uint32_t* rc = (const uint32_t*)(blob + hd->pad1[1]);
+    const TreeFold* tf = (const TreeFold*)(blob + hd->pad1[2]);
+    uint64_t x = seed * 0x9E3779B97F4A7C15ull + 7ull;
+    auto rnd = [&]() {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        return x;
+    };
+    int64_t bad = 0, shaped = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const bool dense = (i & 3) == 0;
+        const uint64_t t[2] = {dense ? rnd() : (rnd() | rnd() | rnd()), dense ? rnd() : (rnd() | rnd() | rnd())};
+        const uint64_t u[2] = {(i & 7) ? (rnd() & rnd() & rnd() & rnd()) : 0ull, (i & 7) ? (rnd() & rnd() & rnd() & rnd()) : 0ull};
+        const uint64_t se[2] = {(i & 5) ? (rnd() & rnd() & rnd() & rnd() & rnd()) : 0ull,
+                                (i & 5) ? (rnd() & rnd() & rnd() & rnd() & rnd()) : 0ull};
+        for (uint32_t k = 0; k < nt; k++) {
+            if (!tf[k].shape) continue;
+            shaped++;
+            int32_t e1, e2;
+            const uint8_t a = run_fold_bits(code + rc[2 * k], rc[2 * k + 1], t, u, se, &e1);
+            const uint8_t b = tree_fold(tf[k], t, u, se, &e2);
+            if (a != b || e1 != e2) bad++;
+        }
+    }
+    return shaped ? bad : -1;
+}
 // group_fold against the code interpreter on n random (T, U, static E) bitmaps of the
 // ruleset's patterns: the number of differences (-1: the ruleset is not kFlagGroupFold)
 extern "C" int64_t ht_group_fold_check(void* h, uint64_t seed, uint32_t n) {

@@ -80,3 +80,34 @@ def test_random_group_folds(ctx, seed):
             docs = [docs[i % len(docs)] for i in range(n)]
             arena, offs, lens = _pack(docs)
             _same(ctx, expr, arena, offs, lens)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_random_forest_tree_folds(ctx, seed):
+    """Forests of flat and two-level trees (TreeFold: each tree folds off its own bits of the
+    128-bit bitmaps, bases on both sides of bit 64) and one three-level tree (interpreted):
+    every tree's result and error index against the oracle of that tree alone."""
+    from authorino_amd import jsonexp as J
+
+    rng = np.random.default_rng(4300 + seed)
+    for _ in range(4):
+        exprs, total = [], 0
+        while total < 80:  # (at most 35 patterns a tree: 115 in all, then 4 more)
+            e = _random_group_expr(rng)
+            exprs.append(e)
+            total += len(e.flatten()[0])
+        p4 = [J.Pattern(s, J.Operator(op), v) for s, op, v in FU.rand_patterns(rng, 4)]
+        exprs.insert(int(rng.integers(0, len(exprs) + 1)), J.All(J.Any(J.All(p4[0], p4[1]), p4[2]), p4[3]))
+        assert sum(len(e.flatten()[0]) for e in exprs) <= 128
+        forest = ctx.compile_forest(exprs)
+        docs = [FU.rand_doc(rng, ws=bool(rng.random() < 0.2)) for _ in range(500)]
+        docs = [docs[i % len(docs)] for i in range(6000)]
+        arena, offs, lens = _pack(docs)
+        ftri, ferr, _ = ctx.eval_host_arena([forest], arena, offs, lens)
+        for k, e in enumerate(exprs):
+            pats, nodes, root = e.flatten()
+            spec = [(p.selector, int(p.operator), p.value) for p in pats]
+            otri, oerr, _ = O.eval_batch([O.Ruleset(spec, nodes, root)], arena, offs, lens, nthreads=8)
+            off = forest.offsets[k]
+            assert np.array_equal(ftri[:, k], otri), k
+            assert np.array_equal(ferr[:, k], np.where(oerr >= 0, oerr + off, -1)), k

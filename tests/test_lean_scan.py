@@ -436,3 +436,57 @@ def test_group_fold_agrees_with_the_code_interpreter(seed):
         tl, _, _, _ = H.eval_lean(hr, w.doc(i), mis=i & 15)
         assert tl == rs.matches(w.doc(i))[0]
     assert L.ht_group_folds() - before >= w.n + n // 2
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_forest_tree_folds_agree_with_the_code_interpreter(seed):
+    """Forest rulesets (one fold program per tree, patterns concatenated by tree): trees of
+    one flat or two-level All / Any carry a TreeFold and fold off their own bits of the
+    128-bit bitmaps (bases across the 64-bit word boundary); tree_fold against the code
+    interpreter on random T / U / static-E bitmaps. c5's forest is one."""
+    import ctypes as C
+
+    from authorino_amd import jsonexp as J
+    from authorino_amd import workloads as W
+
+    L = H.lib()
+    L.ht_tree_fold_check.restype = C.c_int64
+    L.ht_tree_fold_check.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32]
+    rng = np.random.default_rng(950 + seed)
+    checked = 0
+    for it in range(25):
+        trees, total = [], 0
+        while total < 110:
+            outer = J.All if rng.random() < 0.5 else J.Any
+            inner = J.Any if outer is J.All else J.All
+            kids = [None if rng.random() < 0.5 else int(rng.integers(2, 6)) for _ in range(int(rng.integers(1, 6)))]
+            npat = sum(1 if k is None else k for k in kids)
+            ps = [J.Pattern(s, J.Operator(op), v) for s, op, v in FU.rand_patterns(rng, npat)]
+            args, i = [], 0
+            for k in kids:
+                if k is None:
+                    args.append(ps[i])
+                    i += 1
+                else:
+                    args.append(inner(*ps[i:i + k]))
+                    i += k
+            e = outer(*args) if len(args) > 1 or rng.random() < 0.5 else args[0]
+            if rng.random() < 0.15:  # a third level: interpreted
+                e = inner(e, outer(*ps[:2])) if npat >= 2 else e
+            trees.append(e.flatten())
+            total += npat
+        if sum(len(p) for p, _, _ in trees) > 128:
+            trees = trees[:-1]
+        hr = H.HostRuleset.forest([([(p.selector, int(p.operator), p.value) for p in pats], nodes, root)
+                                   for pats, nodes, root in trees])
+        bad = L.ht_tree_fold_check(hr._h, it + 100 * seed, 3000)
+        if bad >= 0:
+            checked += 1
+            assert bad == 0, it
+    assert checked >= 20
+    w = W.make("c5", n=16)
+    ac = w.auth_config
+    ex = [ac.conditions] + [e for c in ac.authorization for e in (c.conditions, c.rules)]
+    hr = H.HostRuleset.forest([([(p.selector, int(p.operator), p.value) for p in pats], nodes, root)
+                               for pats, nodes, root in (e.flatten() for e in ex)])
+    assert L.ht_tree_fold_check(hr._h, 5 + seed, 20000) == 0
